@@ -1,0 +1,181 @@
+/*
+ * mpcmmd.h -- C ABI of libmpcmmd.so, the MI355X (gfx950) implementation of the
+ * MMD / CVaR / SAA CEM-projection optimizer of Basant1861/MPC-MMD.
+ *
+ * The reference has no native code and no FFI: its optimizer is the Python
+ * class `CEM` in synthetic_static_obs/optimizer/cem.py (pure JAX).  This ABI is
+ * what that class's drop-in replacement (mpc-mmd_amd/optimizer/cem.py) binds
+ * through ctypes; each entry point names the reference interface it replaces.
+ * Plain C types only: no torch / HIP types in any signature (a stream is a
+ * `void*` holding a hipStream_t).
+ *
+ * Threading: a handle is bound to one HIP device and one stream and is not
+ * thread-safe; use one handle per thread / GPU.  Every call returns an int
+ * status (0 = ok, < 0 = error; mpcmmd_last_error() has the message, thread
+ * local).
+ */
+#ifndef MPCMMD_H
+#define MPCMMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCMMD_ABI_VERSION 1
+
+/* status codes */
+#define MPCMMD_OK 0
+#define MPCMMD_E_INVALID (-1)     /* bad argument / shape */
+#define MPCMMD_E_HIP (-2)         /* HIP runtime error (message has details) */
+#define MPCMMD_E_UNSUPPORTED (-3) /* configuration outside what is built */
+#define MPCMMD_E_STATE (-4)       /* call order (e.g. iterate before begin) */
+
+/* cost variants: CEM.compute_cem_{mmd_opt,mmd_random,cvar,saa}
+ * (synthetic_static_obs/optimizer/cem.py:201,335,464,590) */
+#define MPCMMD_COST_MMD_OPT 0
+#define MPCMMD_COST_MMD_RANDOM 1
+#define MPCMMD_COST_CVAR 2
+#define MPCMMD_COST_SAA 3
+
+/* noise models: Helper noise=="gaussian" / else beta (optimizer/cem_helper.py:405) */
+#define MPCMMD_NOISE_GAUSSIAN 0
+#define MPCMMD_NOISE_BETA 1
+
+/* scenario constants: synthetic_static_obs vs synthetic_dynamic_obs
+ * (y_lb,y_ub at optimizer/cem.py:155; K_steer at optimizer/cem_helper.py:24) */
+#define MPCMMD_VARIANT_STATIC 0
+#define MPCMMD_VARIANT_DYNAMIC 1
+
+/* Replaces CEM.__init__(num_reduced, num_obs, noise_level, num_prime, noise,
+ * acc_const_noise, steer_const_noise) (optimizer/cem.py:17-18).  num_batch is
+ * the reference's hard-coded 100 (cem.py:137) made configurable. */
+typedef struct mpcmmd_config {
+  int32_t num_reduced;     /* n: samples per candidate (baseline) / reduced set (mmd_opt) */
+  int32_t num_obs;         /* O */
+  float noise_level;       /* sigma_acc = sigma_steer (cem.py:168-169) */
+  int32_t num_prime;       /* H: rollout horizon */
+  int32_t noise;           /* MPCMMD_NOISE_* */
+  float acc_const_noise;
+  float steer_const_noise;
+  int32_t num_batch;       /* B (reference: 100) */
+  int32_t variant;         /* MPCMMD_VARIANT_* */
+  int32_t maxiter_cem;     /* outer CEM iterations (reference: 20, cem.py:89) */
+  int32_t device;          /* HIP device ordinal */
+  uint32_t seed;           /* key word 1 of the internal Philox streams */
+} mpcmmd_config;
+
+/* External draws (the parity contract): every standard normal the solve
+ * consumes, host fp32 row-major.  A NULL field selects the internal Philox
+ * stream for that tensor.  Shapes (T = maxiter_cem, S = num_reduced,
+ * M = num_reduced^2):
+ *   pop0     [B][8]             sampling_param, fixed key      (cem_helper.py:122-150)
+ *   roll     [T][3][S][H]       acc / steer / const noise rows (cem_helper.py:405-441)
+ *   resample [T][B-5][8]        compute_shifted_samples        (cem_helper.py:292)
+ *   beta_z0  [100][M+1]         beta-CEM initial samples       (compute_beta.py:41-49)
+ *   beta_z   [20][89][M+1]      beta-CEM resamples             (compute_beta.py:63)
+ * Beta noise depends on the controls and is always internal. */
+typedef struct mpcmmd_draws {
+  const float* pop0;
+  const float* roll;
+  const float* resample;
+  const float* beta_z0;
+  const float* beta_z;
+} mpcmmd_draws;
+
+/* Return of compute_cem_* (cem.py:324-333 / 456-462): the obstacle-cost
+ * elite 0 of the LAST outer iteration.  beta must point to >= n floats for
+ * mmd_opt (may be NULL otherwise).  The trace pointers are optional (NULL =
+ * not copied) and receive per-iteration elite index sets for parity tests:
+ * elite_proj [T][B] (argsort of res_norm), elite_obs [T][20] (candidate
+ * indices), elite_cem [T][5] (indices into the 20). */
+typedef struct mpcmmd_result {
+  float cx[11];
+  float cy[11];
+  float cost_lane;
+  float cost_obs;
+  float sigma;          /* mmd_opt */
+  float res_beta[20];   /* mmd_opt */
+  float* beta;          /* [n], mmd_opt */
+  int32_t* elite_proj;
+  int32_t* elite_obs;
+  int32_t* elite_cem;
+} mpcmmd_result;
+
+typedef struct mpcmmd_handle mpcmmd_handle;
+
+int32_t mpcmmd_abi_version(void);
+const char* mpcmmd_last_error(void);
+
+/* Number of visible HIP devices (0 when none; never fails). */
+int32_t mpcmmd_device_count(void);
+
+/* CEM.__init__: allocates every device buffer and uploads the
+ * batch-invariant matrices.  No allocation happens after this. */
+int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out);
+void mpcmmd_destroy(mpcmmd_handle* h);
+
+/* Run on a caller-owned hipStream_t instead of the handle's own stream. */
+int mpcmmd_set_stream(mpcmmd_handle* h, void* hip_stream);
+void* mpcmmd_get_stream(mpcmmd_handle* h);
+
+/* CEM.compute_cem_{mmd_opt,mmd_random,cvar,saa}(idx_mpc, init_state,
+ * mean_param_init, cov_param_init, x_obs_traj, y_obs_traj, v_des)
+ * (cem.py:201-204 etc.).  x_obs / y_obs are [O][100] row-major.  draws may
+ * be NULL (internal RNG).  Synchronous. */
+int mpcmmd_solve(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const float init_state[6],
+                 const float mean[8], const float cov[64], const float* x_obs, const float* y_obs,
+                 float v_des, const mpcmmd_draws* draws, mpcmmd_result* out);
+
+/* The same solve in three steps (what mpcmmd_solve does), for callers that
+ * time or interleave work: begin uploads inputs and builds the initial carry
+ * (sampling_param, compute_boundary_vec; cem.py:206-219); iterate enqueues
+ * outer iterations [t_begin, t_begin+count) (the lax_cem body, cem.py:221-315)
+ * asynchronously on the handle's stream; finish synchronises and downloads
+ * the result of the last enqueued iteration. */
+int mpcmmd_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const float init_state[6],
+                 const float mean[8], const float cov[64], const float* x_obs, const float* y_obs,
+                 float v_des, const mpcmmd_draws* draws);
+int mpcmmd_iterate(mpcmmd_handle* h, int32_t t_begin, int32_t count);
+int mpcmmd_finish(mpcmmd_handle* h, mpcmmd_result* out);
+int mpcmmd_sync(mpcmmd_handle* h);
+
+/* Per-kernel HIP-event timing (on the handle's stream).  When enabled, every
+ * launch of every kernel is bracketed by events; mpcmmd_kernel_times returns,
+ * per kernel id, the number of launches and the total milliseconds since the
+ * last reset.  Kernel ids: see mpcmmd_kernel_name. */
+int mpcmmd_profile(mpcmmd_handle* h, int32_t enable);
+int mpcmmd_kernel_times(mpcmmd_handle* h, int32_t* launches, double* total_ms, int32_t max_kernels);
+const char* mpcmmd_kernel_name(int32_t id);
+
+/* Named device buffers, for stage-level parity tests (read / overwrite the
+ * scan carry and intermediates between stages).  Names and sizes: see
+ * mpcmmd_buffer_info. */
+int mpcmmd_buffer_info(mpcmmd_handle* h, const char* name, size_t* bytes);
+int mpcmmd_read(mpcmmd_handle* h, const char* name, void* dst, size_t bytes);
+int mpcmmd_write(mpcmmd_handle* h, const char* name, const void* src, size_t bytes);
+
+/* Stage entry points: run one kernel of iteration t on the current device
+ * state (the stages mpcmmd_iterate chains):
+ *   0 noise      (internal RNG draws of iteration t)
+ *   1 front      compute_x_guess + compute_projection + compute_controls
+ *                (cem_helper.py:169-230, projection.py:276-323, cem_helper.py:540-551)
+ *   2 risk       noisy rollouts + collision residual + risk reducer per candidate
+ *                (cem_helper.py:402-538, costs.py:50-234, compute_beta.py:93-157)
+ *   3 select     argsorts, compute_cost, elites, compute_shifted_samples
+ *                (cem.py:233-315, cem_helper.py:232-314) */
+int mpcmmd_run_stage(mpcmmd_handle* h, int32_t stage, int32_t t);
+
+/* Host-side batch-invariant constants (no GPU needed): fills dst with the
+ * fp64 values of `name` ("P","Pdot","Pddot" [100][11] (fp32-rounded),
+ * "P_prime" [H][11], "guess_kinv_x" [14][14], "guess_kinv_y" [15][15],
+ * "proj_kinv_x", "proj_kinv_y", "fit" [11][H]).  Returns element count, or
+ * < 0 on error / when count is too small. */
+int mpcmmd_host_constant(const mpcmmd_config* cfg, const char* name, double* dst, size_t count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCMMD_H */

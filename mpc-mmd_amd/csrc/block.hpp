@@ -1,0 +1,149 @@
+// Workgroup-level helpers: reductions, bitonic sort of 64-bit keys in LDS,
+// and the CVaR / SAA / MMD reducers over an LDS-resident sample vector.
+#pragma once
+#include "common.hpp"
+
+namespace mpcmmd {
+
+// sum over the workgroup (blockDim.x multiple of 64); scratch: >= 16 doubles
+DEVI double block_sum(double v, double* scratch) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) scratch[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < nw; ++i) s += scratch[i];
+  __syncthreads();
+  return s;
+}
+DEVI int block_sum(int v, int* scratch) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) scratch[w] = v;
+  __syncthreads();
+  int s = 0;
+  for (int i = 0; i < nw; ++i) s += scratch[i];
+  __syncthreads();
+  return s;
+}
+
+// ascending bitonic sort of N (power of two) 64-bit keys in LDS, whole block
+DEVI void bitonic_sort(unsigned long long* k, int N) {
+  for (int size = 2; size <= N; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < (N >> 1); i += blockDim.x) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const unsigned long long a = k[lo], b = k[hi];
+        if ((a > b) == up) {
+          k[lo] = b;
+          k[hi] = a;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+struct ReduceScratch {
+  double d[16];
+  int i[16];
+  int list_n;
+  float v_lo, v_hi;
+};
+
+// jnp.quantile(x, 0.98) (linear, JAX fp32 weights) + mean of the tail
+// (costs.py:215-219) over vals[0..S).  list: >= S ints of LDS scratch.
+// Sorted order = the jnp.argsort total order (ties by index).
+DEVI float block_cvar(const float* vals, int S, int* list, ReduceScratch& rs) {
+  const float pos = 0.98f * float(S - 1);
+  const float flo = floorf(pos), fhi = ceilf(pos);
+  const float hw = pos - flo;
+  const float lw = 1.0f - hw;
+  const int lo = min(max(int(flo), 0), S - 1), hi = min(max(int(fhi), 0), S - 1);
+  if (threadIdx.x == 0) rs.list_n = 0;
+  __syncthreads();
+  // zero class (key of +-0) sorts first: count it, compact the rest
+  int nz = 0;
+  for (int s = threadIdx.x; s < S; s += blockDim.x) {
+    if (sort_key(vals[s]) == 0x80000000u) {
+      ++nz;
+    } else {
+      const int slot = atomicAdd(&rs.list_n, 1);
+      list[slot] = s;
+    }
+  }
+  const int z = block_sum(nz, rs.i);  // also a barrier
+  const int m = rs.list_n;
+  if (threadIdx.x == 0) {
+    rs.v_lo = 0.0f;
+    rs.v_hi = 0.0f;
+  }
+  __syncthreads();
+  if (hi >= z) {
+    for (int a = threadIdx.x; a < m; a += blockDim.x) {
+      const int ia = list[a];
+      const uint32_t ka = sort_key(vals[ia]);
+      int r = 0;
+      for (int c = 0; c < m; ++c) {
+        const int ic = list[c];
+        const uint32_t kc = sort_key(vals[ic]);
+        r += (kc < ka) || (kc == ka && ic < ia);
+      }
+      if (r == lo - z) rs.v_lo = vals[ia];
+      if (r == hi - z) rs.v_hi = vals[ia];
+    }
+  }
+  __syncthreads();
+  const float var = rs.v_lo * lw + rs.v_hi * hw;
+  double sum = 0.0;
+  int cnt = 0;
+  for (int s = threadIdx.x; s < S; s += blockDim.x) {
+    const float v = vals[s];
+    if (v >= var) {  // false for NaN
+      sum += double(v);
+      ++cnt;
+    }
+  }
+  sum = block_sum(sum, rs.d);
+  cnt = block_sum(cnt, rs.i);
+  return cnt > 0 ? float(sum / double(cnt)) : 0.0f;
+}
+
+// fraction of samples > 0 (costs.py:230-234, 160-171)
+DEVI int block_count_pos(const float* vals, int S, ReduceScratch& rs) {
+  int c = 0;
+  for (int s = threadIdx.x; s < S; s += blockDim.x) c += vals[s] > 0.0f;
+  return block_sum(c, rs.i);
+}
+
+// Laplace-kernel MMD against a Dirac at 0 (kernel_computation.py:67-87):
+// ker_wt (b^T K_aa b - 2 b^T K_ab b_del) with K = exp(-|d| / sigma).
+// beta == nullptr means uniform beta = float32(1/n) (mmd_random, cem.py:355).
+DEVI float block_mmd(const float* c, const float* beta, int n, float sigma, float ker_wt, ReduceScratch& rs) {
+  const float bdel = 1.0f / float(n);
+  const float rs_sig = 1.0f / sigma;
+  double q1 = 0.0, q2 = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float ci = c[i];
+    double row = 0.0;
+    for (int k = 0; k < n; ++k) {
+      const float d = fabsf(ci - c[k]);
+      const float kk = __expf(div_rc(-d, sigma, rs_sig));
+      row += double(kk) * double(beta ? beta[k] : bdel);
+    }
+    const double bi = double(beta ? beta[i] : bdel);
+    q1 += bi * row;
+    const float kab = __expf(div_rc(-fabsf(ci - 0.0f), sigma, rs_sig));
+    q2 += bi * (double(kab) * (double(n) * double(bdel)));
+  }
+  q1 = block_sum(q1, rs.d);
+  q2 = block_sum(q2, rs.d);
+  return float(double(ker_wt) * (q1 - 2.0 * q2));
+}
+
+}  // namespace mpcmmd

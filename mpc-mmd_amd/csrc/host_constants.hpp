@@ -1,0 +1,57 @@
+// Batch-invariant constants of the optimizer, computed on the host in fp64.
+// Restates CEM.__init__ / Helper.__init__ (synthetic_static_obs/optimizer/
+// cem.py:17-199, cem_helper.py:10-120) and the matrices the reference rebuilds
+// inside every jitted call (guess QP cem_helper.py:207-217, projection KKT
+// projection.py:145-156, Bernstein fit cem_helper.py:556).  The reference
+// solves each of these batch-invariant systems with an fp32 LU per call; here
+// they are inverted once in fp64 and applied as fp64 GEMVs on the device.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace mpcmmd {
+
+constexpr int kNum = 100;   // planning points (cem.py:38)
+constexpr int kNvar = 11;   // Bernstein degree 10 (cem.py:50)
+constexpr int kLane = 2 * (kNum - 1);
+
+struct ProblemConsts {
+  // scalars (Appendix B of SURVEY.md)
+  double a_obs = 4.25, b_obs = 2.75, wheel_base = 2.5;
+  double v_min = 0.1, v_max = 30.0, a_max = 18.0, steer_max = 0.6;
+  double t_fin = 15.0, dt = 0.15;
+  double k_p_v = 2.0, k_p = 2.0;
+  double y_lb = -2.25, y_ub = 2.25, K_steer = 0.01;
+  double alpha_mean = 0.6, alpha_cov = 0.6, lamda = 0.9;
+  double ker_wt = 1000.0, alpha_quant = 0.98;
+  int H = 0;
+  // fp32-rounded basis, stored as double [100][11]
+  std::vector<double> P, Pd, Pdd;
+  std::vector<double> P64, Pd64, Pdd64;   // unrounded (the reference's self.P etc.)
+  std::vector<double> P_prime;            // [H][11], fp32-rounded
+  std::vector<double> guess_kinv_x;       // [14][14]
+  std::vector<double> guess_kinv_y;       // [15][15]
+  std::vector<double> guess_colsum_x;     // [4][11]
+  std::vector<double> guess_colsum_y;     // [4][11]
+  std::vector<double> proj_kinv_x;        // [14][14]
+  std::vector<double> proj_kinv_y;        // [15][15]
+  std::vector<double> fit;                // [11][H] = (P'^T P' + 0.05 I)^-1 P'^T
+};
+
+// variant: 0 static, 1 dynamic.  Throws std::runtime_error on a singular
+// matrix (never for valid H >= 2).
+ProblemConsts build_constants(int num_prime, int variant);
+
+// numpy.linspace(start, stop, num) (fp64, endpoint included).
+std::vector<double> linspace(double start, double stop, int num);
+
+// Bernstein degree-10 basis on grid t, same operation order as
+// oracle/problem.py:bernstein_order10 (so the two agree bit for bit).
+void bernstein10(const std::vector<double>& t, double tmin, double tmax, std::vector<double>& P,
+                 std::vector<double>& Pd, std::vector<double>& Pdd);
+
+// In-place Gauss-Jordan inverse with partial pivoting (n x n, row-major).
+bool invert(std::vector<double>& a, int n);
+
+}  // namespace mpcmmd

@@ -1,0 +1,383 @@
+// Stage "front": initial guess QP + one ADMM projection iteration + controls,
+// one wave64 per candidate, 4 candidates per 256-thread workgroup.
+//
+//   compute_x_guess      optimizer/cem_helper.py:169-230
+//   compute_projection   optimizer/projection.py:276-323
+//     initial_alpha_d_obs  :52-121   (obstacle terms dead)
+//     compute_x            :123-185
+//     compute_alph_d       :193-274
+//   compute_controls     optimizer/cem_helper.py:540-551
+//
+// Lane l owns planning points t = l and t = l + 64 (< 100).  The 100x11
+// Bernstein bases are staged once per workgroup in LDS (13.2 KB).  Every
+// basis product P c / P^T r accumulates in fp64 and is rounded to fp32 where
+// the reference holds an fp32 array; the batch-invariant KKT solves are fp64
+// GEMVs with inverses built on the host (host_constants.cpp).  Elementwise
+// work is fp32 in the reference's operation order (-ffp-contract=off).
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace mpcmmd {
+
+namespace {
+
+constexpr int kN = 100;
+constexpr int kNv = 11;
+constexpr float kPiF = 3.14159274101257324f;     // float32(pi)
+constexpr float kTwoPiF = 6.28318548202514648f;  // float32(2 pi)
+
+struct Rows {
+  float P[2][kNv], D[2][kNv], DD[2][kNv];
+};
+
+DEVI float eval_row(const float (&r)[kNv], const double (&c)[kNv]) {
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < kNv; ++k) s += double(r[k]) * c[k];
+  return float(s);
+}
+
+// out[k] = fp32( sum_t M[t][k] r[t] ) over the wave's 100 points
+DEVI void adj(const float (&M0)[kNv], float r0, const float (&M1)[kNv], float r1, bool v1, float (&out)[kNv]) {
+#pragma unroll
+  for (int k = 0; k < kNv; ++k) {
+    double s = double(M0[k]) * double(r0);
+    if (v1) s += double(M1[k]) * double(r1);
+    out[k] = float(wave_sum(s));
+  }
+}
+
+// jnp.remainder(x, 2pi) for the unwrap (fmod, then shift into [0, 2pi))
+DEVI float rem_2pi(float x) {
+  float r = fmodf(x, kTwoPiF);
+  if (r != 0.0f && r < 0.0f) r = r + kTwoPiF;
+  return r;
+}
+
+// per-step phase correction of jnp.unwrap (period 2 pi, discont pi)
+DEVI float unwrap_corr(float dd) {
+  float ddmod = rem_2pi(dd + kPiF) - kPiF;
+  if (ddmod == -kPiF && dd > 0.0f) ddmod = kPiF;
+  return fabsf(dd) < kPiF ? 0.0f : ddmod - dd;
+}
+
+// alpha = unwrap(atan2) along the 100 points; lane owns t0 = lane, t1 = lane + 64
+DEVI void unwrap2(float& a0, float& a1, int lane, bool v1) {
+  const float prev0 = __shfl_up(a0, 1, kWave);
+  const float last0 = readlane_f(a0, 63);
+  const float up1 = __shfl_up(a1, 1, kWave);  // shuffles outside any divergent branch
+  const float prev1 = lane == 0 ? last0 : up1;
+  const float ph0 = lane == 0 ? 0.0f : unwrap_corr(a0 - prev0);
+  const float ph1 = v1 ? unwrap_corr(a1 - prev1) : 0.0f;
+  // sequential cumsum (numpy / oracle order)
+  float acc = 0.0f, cs0 = 0.0f, cs1 = 0.0f;
+#pragma unroll
+  for (int i = 1; i < 64; ++i) {
+    acc = acc + readlane_f(ph0, i);
+    cs0 = lane == i ? acc : cs0;
+  }
+#pragma unroll
+  for (int i = 0; i < kN - 64; ++i) {
+    acc = acc + readlane_f(ph1, i);
+    cs1 = lane == i ? acc : cs1;
+  }
+  if (lane > 0) a0 = a0 + cs0;
+  if (v1) a1 = a1 + cs1;
+}
+
+// Correctly rounded fp32 transcendentals (fp64 evaluation, one rounding).
+// The oracle does the same (oracle/helper.py: cr): feasible candidates'
+// res_norm is rounding noise, so reproducible transcendentals are what makes
+// the projection-elite order reproducible (DESIGN.md Numerics).
+DEVI float cr_atan2(float y, float x) { return float(atan2(double(y), double(x))); }
+DEVI float cr_cos(float a) { return float(cos(double(a))); }
+DEVI float cr_sin(float a) { return float(sin(double(a))); }
+
+struct Polar {
+  float ca, sa, d;
+};
+
+// alpha = atan2(wy, wx); d = clip((wx cos + wy sin) / (cos^2 + sin^2), lo, hi)
+DEVI Polar polar_of(float alpha, float wx, float wy, float lo, float hi) {
+  const float ca = cr_cos(alpha), sa = cr_sin(alpha);
+  const float c1 = ca * ca + sa * sa;
+  const float c2 = wx * ca + wy * sa;
+  float d = c2 / c1;
+  d = fminf(fmaxf(d, lo), hi);
+  return Polar{ca, sa, d};
+}
+
+__global__ __launch_bounds__(256) void k_front(Params p, int t) {
+  __shared__ float sB[3 * kN * kNv];
+  for (int i = threadIdx.x; i < 3 * kN * kNv; i += blockDim.x) sB[i] = p.basis[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= p.B) return;
+  const int t0 = lane, t1 = lane + 64;
+  const bool v1 = t1 < kN;
+  const int t1c = v1 ? t1 : kN - 1;
+  Rows R;
+#pragma unroll
+  for (int k = 0; k < kNv; ++k) {
+    R.P[0][k] = sB[0 * kN * kNv + t0 * kNv + k];
+    R.P[1][k] = sB[0 * kN * kNv + t1c * kNv + k];
+    R.D[0][k] = sB[1 * kN * kNv + t0 * kNv + k];
+    R.D[1][k] = sB[1 * kN * kNv + t1c * kNv + k];
+    R.DD[0][k] = sB[2 * kN * kNv + t0 * kNv + k];
+    R.DD[1][k] = sB[2 * kN * kNv + t1c * kNv + k];
+  }
+
+  // ---- compute_x_guess: c_bar = G v + h (fp64) -------------------------------
+  const float* pop = p.pop + (size_t(t & 1) * p.B + b) * 8;
+  double cxb[kNv], cyb[kNv];
+  float fcxb[kNv], fcyb[kNv];
+  {
+    double v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = double(pop[j]);
+#pragma unroll
+    for (int k = 0; k < kNv; ++k) {
+      double sx = p.solve_c[0 * kNv + k], sy = p.solve_c[1 * kNv + k];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sx += p.guess_g[(0 * kNv + k) * 4 + j] * v[j];
+        sy += p.guess_g[(1 * kNv + k) * 4 + j] * v[4 + j];
+      }
+      fcxb[k] = float(sx);
+      fcyb[k] = float(sy);
+      cxb[k] = double(fcxb[k]);
+      cyb[k] = double(fcyb[k]);
+    }
+  }
+
+  // ---- initial_alpha_d_obs (projection.py:52-121) ----------------------------
+  float xd[2], yd[2], xdd[2], ydd[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    xd[q] = eval_row(R.D[q], cxb);
+    yd[q] = eval_row(R.D[q], cyb);
+    xdd[q] = eval_row(R.DD[q], cxb);
+    ydd[q] = eval_row(R.DD[q], cyb);
+  }
+  float av0 = cr_atan2(yd[0], xd[0]), av1 = cr_atan2(yd[1], xd[1]);
+  float aa0 = cr_atan2(ydd[0], xdd[0]), aa1 = cr_atan2(ydd[1], xdd[1]);
+  unwrap2(av0, av1, lane, v1);
+  unwrap2(aa0, aa1, lane, v1);
+  Polar pv[2] = {polar_of(av0, xd[0], yd[0], 0.1f, 30.0f), polar_of(av1, xd[1], yd[1], 0.1f, 30.0f)};
+  Polar pa[2] = {polar_of(aa0, xdd[0], ydd[0], 0.0f, 18.0f), polar_of(aa1, xdd[1], ydd[1], 0.0f, 18.0f)};
+
+  float lx[kNv], ly[kNv], tmp[kNv], tmp2[kNv];
+#pragma unroll
+  for (int k = 0; k < kNv; ++k) {
+    lx[k] = p.lam_x[size_t(b) * kNv + k];
+    ly[k] = p.lam_y[size_t(b) * kNv + k];
+  }
+  {
+    float rax[2], ray[2], rvx[2], rvy[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      rax[q] = xdd[q] - pa[q].d * pa[q].ca;
+      ray[q] = ydd[q] - pa[q].d * pa[q].sa;
+      rvx[q] = xd[q] - pv[q].d * pv[q].ca;
+      rvy[q] = yd[q] - pv[q].d * pv[q].sa;
+    }
+    adj(R.DD[0], rax[0], R.DD[1], rax[1], v1, tmp);
+    adj(R.D[0], rvx[0], R.D[1], rvx[1], v1, tmp2);
+#pragma unroll
+    for (int k = 0; k < kNv; ++k) lx[k] = (lx[k] - tmp[k]) - tmp2[k];
+    adj(R.DD[0], ray[0], R.DD[1], ray[1], v1, tmp);
+    adj(R.D[0], rvy[0], R.D[1], rvy[1], v1, tmp2);
+#pragma unroll
+    for (int k = 0; k < kNv; ++k) ly[k] = (ly[k] - tmp[k]) - tmp2[k];
+  }
+
+  // ---- compute_x (projection.py:123-185) --------------------------------------
+  // lane-bound rows j = t-1 (t = 1..99): ub row j, lb row 99 + j; A_lane = [P[1:]; -P[1:]]
+  const float y_ub = p.y_ub, mlb = -p.y_lb;  // b_lane: ub rows y_ub, lb rows -y_lb (gamma = 1)
+  float* sl = p.s_lane + size_t(b) * (2 * (kN - 1));
+  const bool h0 = t0 >= 1;  // t0 = 0 has no lane row
+  float baug_ub[2] = {0.f, 0.f}, baug_lb[2] = {0.f, 0.f};
+  if (h0) {
+    baug_ub[0] = y_ub - sl[t0 - 1];
+    baug_lb[0] = mlb - sl[kN - 1 + t0 - 1];
+  }
+  if (v1) {
+    baug_ub[1] = y_ub - sl[t1 - 1];
+    baug_lb[1] = mlb - sl[kN - 1 + t1 - 1];
+  }
+  float cx[kNv], cy[kNv];
+  {
+    float bx[2], by[2], vxb[2], vyb[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      bx[q] = pa[q].d * pa[q].ca;
+      by[q] = pa[q].d * pa[q].sa;
+      vxb[q] = pv[q].d * pv[q].ca;
+      vyb[q] = pv[q].d * pv[q].sa;
+    }
+    float linx[kNv], liny[kNv];
+    adj(R.DD[0], bx[0], R.DD[1], bx[1], v1, tmp);
+    adj(R.D[0], vxb[0], R.D[1], vxb[1], v1, tmp2);
+#pragma unroll
+    for (int k = 0; k < kNv; ++k) linx[k] = ((-lx[k] - fcxb[k]) - tmp[k]) - tmp2[k];
+    adj(R.DD[0], by[0], R.DD[1], by[1], v1, tmp);
+    adj(R.D[0], vyb[0], R.D[1], vyb[1], v1, tmp2);
+#pragma unroll
+    for (int k = 0; k < kNv; ++k) liny[k] = ((-ly[k] - fcyb[k]) - tmp[k]) - tmp2[k];
+    // A_lane^T b_aug: sum_j P[j+1][k] (baug_ub[j] - baug_lb[j]) in fp64
+#pragma unroll
+    for (int k = 0; k < kNv; ++k) {
+      double s = 0.0;
+      if (h0) s += double(R.P[0][k]) * double(baug_ub[0]) - double(R.P[0][k]) * double(baug_lb[0]);
+      if (v1) s += double(R.P[1][k]) * double(baug_ub[1]) - double(R.P[1][k]) * double(baug_lb[1]);
+      liny[k] = liny[k] - float(wave_sum(s));
+    }
+    // KKT solve: c = Kinv[:11,:11] (-lincost) + Kinv[:11,11:] b_eq
+#pragma unroll
+    for (int k = 0; k < kNv; ++k) {
+      double sx = p.solve_c[2 * kNv + k], sy = p.solve_c[3 * kNv + k];
+#pragma unroll
+      for (int j = 0; j < kNv; ++j) {
+        sx += p.proj_m[(0 * kNv + k) * kNv + j] * (-double(linx[j]));
+        sy += p.proj_m[(1 * kNv + k) * kNv + j] * (-double(liny[j]));
+      }
+      cx[k] = float(sx);
+      cy[k] = float(sy);
+    }
+  }
+  double dcx[kNv], dcy[kNv];
+#pragma unroll
+  for (int k = 0; k < kNv; ++k) {
+    dcx[k] = double(cx[k]);
+    dcy[k] = double(cy[k]);
+  }
+  float x[2], y[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    x[q] = eval_row(R.P[q], dcx);
+    y[q] = eval_row(R.P[q], dcy);
+    xd[q] = eval_row(R.D[q], dcx);
+    yd[q] = eval_row(R.D[q], dcy);
+    xdd[q] = eval_row(R.DD[q], dcx);
+    ydd[q] = eval_row(R.DD[q], dcy);
+  }
+  // s_lane / res_lane (A_lane c_y = [y[1:]; -y[1:]])
+  float rl_ub[2] = {0.f, 0.f}, rl_lb[2] = {0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const bool ok = q == 0 ? h0 : v1;
+    if (!ok) continue;
+    const int j = (q == 0 ? t0 : t1) - 1;
+    const float ac_ub = y[q], ac_lb = -y[q];
+    const float s_ub = fmaxf(0.0f, -ac_ub + y_ub);
+    const float s_lb = fmaxf(0.0f, -ac_lb + mlb);
+    rl_ub[q] = (ac_ub - y_ub) + s_ub;
+    rl_lb[q] = (ac_lb - mlb) + s_lb;
+    sl[j] = s_ub;
+    sl[kN - 1 + j] = s_lb;
+  }
+
+  // ---- compute_alph_d (projection.py:193-274), no unwrap (Q13) ---------------
+  Polar qv[2], qa[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    qv[q] = polar_of(cr_atan2(yd[q], xd[q]), xd[q], yd[q], 0.1f, 30.0f);
+    qa[q] = polar_of(cr_atan2(ydd[q], xdd[q]), xdd[q], ydd[q], 0.0f, 18.0f);
+  }
+  float rax[2], ray[2], rvx[2], rvy[2];
+  double n_acc = 0.0, n_vel = 0.0, n_lane = 0.0;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    rax[q] = xdd[q] - qa[q].d * qa[q].ca;
+    ray[q] = ydd[q] - qa[q].d * qa[q].sa;
+    rvx[q] = xd[q] - qv[q].d * qv[q].ca;
+    rvy[q] = yd[q] - qv[q].d * qv[q].sa;
+    const bool ok = q == 0 ? true : v1;
+    if (ok) {
+      n_acc += double(rax[q]) * double(rax[q]) + double(ray[q]) * double(ray[q]);
+      n_vel += double(rvx[q]) * double(rvx[q]) + double(rvy[q]) * double(rvy[q]);
+      n_lane += double(rl_ub[q]) * double(rl_ub[q]) + double(rl_lb[q]) * double(rl_lb[q]);
+    }
+  }
+  n_acc = wave_sum(n_acc);
+  n_vel = wave_sum(n_vel);
+  n_lane = wave_sum(n_lane);
+  const float rn = (float(sqrt(n_acc)) + float(sqrt(n_vel))) + float(sqrt(n_lane));
+  adj(R.DD[0], rax[0], R.DD[1], rax[1], v1, tmp);
+  adj(R.D[0], rvx[0], R.D[1], rvx[1], v1, tmp2);
+#pragma unroll
+  for (int k = 0; k < kNv; ++k) lx[k] = (lx[k] - tmp[k]) - tmp2[k];
+  adj(R.DD[0], ray[0], R.DD[1], ray[1], v1, tmp);
+  adj(R.D[0], rvy[0], R.D[1], rvy[1], v1, tmp2);
+#pragma unroll
+  for (int k = 0; k < kNv; ++k) {
+    double s = 0.0;
+    if (h0) s += double(R.P[0][k]) * double(rl_ub[0]) - double(R.P[0][k]) * double(rl_lb[0]);
+    if (v1) s += double(R.P[1][k]) * double(rl_ub[1]) - double(R.P[1][k]) * double(rl_lb[1]);
+    ly[k] = ((ly[k] - tmp[k]) - tmp2[k]) - float(wave_sum(s));
+  }
+
+  // ---- compute_controls (cem_helper.py:540-551) ------------------------------
+  float v[2], accv[2], steer[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) v[q] = sqrtf(xd[q] * xd[q] + yd[q] * yd[q]);
+  {
+    const float d0 = __shfl_down(v[0], 1, kWave);
+    const float first1 = readlane_f(v[1], 0);
+    const float n1 = __shfl_down(v[1], 1, kWave);
+    const float nxt0 = lane < 63 ? d0 : first1;
+    const float nxt1 = (t1 == kN - 1) ? v[1] : n1;
+    accv[0] = (nxt0 - v[0]) / 0.15f;
+    accv[1] = (nxt1 - v[1]) / 0.15f;
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const float s2 = xd[q] * xd[q] + yd[q] * yd[q];
+    const float curv = (ydd[q] * xd[q] - yd[q] * xdd[q]) / float(pow(double(s2), 1.5));
+    steer[q] = float(atan(double(curv * 2.5f)));
+  }
+
+  // ---- stores -----------------------------------------------------------------
+  float* tr = p.traj;
+  const size_t plane = size_t(p.B) * kN;
+  const size_t row = size_t(b) * kN;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (q == 1 && !v1) break;
+    const int tt = q == 0 ? t0 : t1;
+    tr[0 * plane + row + tt] = x[q];
+    tr[1 * plane + row + tt] = y[q];
+    tr[2 * plane + row + tt] = xd[q];
+    tr[3 * plane + row + tt] = yd[q];
+    tr[4 * plane + row + tt] = xdd[q];
+    tr[5 * plane + row + tt] = ydd[q];
+    p.acc[row + tt] = accv[q];
+    p.steer[row + tt] = steer[q];
+  }
+  if (lane < kNv) {
+    // lane k stores component k (every lane holds all 11 in registers)
+    float vcx = 0.f, vcy = 0.f, vlx = 0.f, vly = 0.f;
+#pragma unroll
+    for (int k = 0; k < kNv; ++k)
+      if (lane == k) {
+        vcx = cx[k];
+        vcy = cy[k];
+        vlx = lx[k];
+        vly = ly[k];
+      }
+    p.cx[size_t(b) * kNv + lane] = vcx;
+    p.cy[size_t(b) * kNv + lane] = vcy;
+    p.lam_x[size_t(b) * kNv + lane] = vlx;
+    p.lam_y[size_t(b) * kNv + lane] = vly;
+  }
+  if (lane == 0) p.res_norm[b] = rn;
+}
+
+}  // namespace
+
+void launch_front(const Params& p, int t, hipStream_t s) {
+  hipLaunchKernelGGL(k_front, dim3((p.B + 3) / 4), dim3(256), 0, s, p, t);
+}
+
+}  // namespace mpcmmd

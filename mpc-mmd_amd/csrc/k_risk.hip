@@ -1,0 +1,179 @@
+// Stage "risk" for the baseline cost variants (cvar, saa, mmd_random): one
+// workgroup per candidate, one thread per noisy rollout sample.
+//
+//   noise injection          optimizer/cem_helper.py:405-443 (gaussian / beta)
+//   compute_rollout_one_step optimizer/cem_helper.py:380-400
+//   H-step scan              optimizer/cem_helper.py:445-461
+//   compute_f_bar + max      optimizer/costs.py:50-60, 210-213
+//   compute_lane_bar + max   optimizer/costs.py:62-71
+//   reducers                 costs.py:206-234 (obs), 137-171 (lane),
+//                            kernel_computation.py:67-87 (mmd_random)
+//
+// The B x S x H rollout planes of the reference are never materialised: each
+// thread keeps its state in registers and folds the collision residual
+// (O obstacles, staged in LDS) and the lane bars into running maxima, so
+// the stage reads only the candidate's H controls and the shared noise rows
+// (L2-resident, [H][S] for coalescing) and writes two floats per candidate.
+#include "block.hpp"
+#include "kernels.hpp"
+#include "rng.hpp"
+
+namespace mpcmmd {
+
+namespace {
+
+constexpr float kA2 = 18.0625f, kB2 = 7.5625f;  // 4.25^2, 2.75^2 (exact in fp32)
+
+struct RiskLds {
+  float* xo;
+  float* yo;
+  float* a;
+  float* st;
+  float* cbar;
+  float* lb;
+  float* ub;
+  int* list;
+  ReduceScratch* rs;
+};
+
+DEVI RiskLds carve(char* base, int O, int H, int S) {
+  RiskLds L;
+  float* f = reinterpret_cast<float*>(base);
+  L.xo = f;
+  f += O * H;
+  L.yo = f;
+  f += O * H;
+  L.a = f;
+  f += H;
+  L.st = f;
+  f += H;
+  L.cbar = f;
+  f += S;
+  L.lb = f;
+  f += S;
+  L.ub = f;
+  f += S;
+  L.list = reinterpret_cast<int*>(f);
+  f += S;
+  size_t off = size_t(reinterpret_cast<char*>(f) - base);
+  off = (off + 15) & ~size_t(15);
+  L.rs = reinterpret_cast<ReduceScratch*>(base + off);
+  return L;
+}
+
+}  // namespace
+
+size_t risk_lds_bytes(int O, int H, int S) {
+  size_t f = size_t(2 * O * H + 2 * H + 4 * S) * 4;
+  f = (f + 15) & ~size_t(15);
+  return f + sizeof(ReduceScratch);
+}
+
+// Noisy controls of sample row r at step h (cem_helper.py:414-443 / 478-508).
+DEVI void noisy_control(const Params& p, int t, int r, int h, float a, float s, float& an, float& sn) {
+  const int S = p.S, H = p.H;
+  const float* roll = p.roll + size_t(t) * 3 * H * S;
+  const float nc = roll[(2 * H + h) * S + r];
+  float ap, sp;
+  if (p.noise == 0) {
+    ap = (p.sigma_acc * fabsf(a)) * roll[(0 * H + h) * S + r];
+    sp = (p.sigma_steer * fabsf(s)) * roll[(1 * H + h) * S + r];
+  } else {
+    const uint32_t k0 = iteration_key0(p.idx_mpc, t), k1 = p.seed;
+    const uint32_t elem = uint32_t(r) * uint32_t(H) + uint32_t(h);
+    const float fa = fabsf(a), fs = fabsf(s);
+    const float nba = beta_draw(double(2.0f * fa), double(5.0f * fa), 2.0, 5.0, k0, k1, kStreamGammaAccA,
+                                kStreamGammaAccB, elem);
+    const float nbs = beta_draw(double(2.0f * fs), double(5.0f * fs), 2.0, 5.0, k0, k1, kStreamGammaSteerA,
+                                kStreamGammaSteerB, elem);
+    ap = p.sigma_acc * (2.0f * nba - 1.0f);
+    sp = p.K_steer * (2.0f * nbs - 1.0f);  // K_steer holds float32(K_steer * sigma_steer)
+  }
+  an = (a + ap) + p.acc_const * nc;
+  sn = (s + sp) + p.steer_const * nc;
+}
+
+namespace {
+
+__global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int O = p.O, H = p.H, S = p.S;
+  RiskLds L = carve(smem, O, H, S);
+  const int b = blockIdx.x;
+  for (int i = threadIdx.x; i < O * H; i += blockDim.x) {
+    L.xo[i] = p.obs[i];
+    L.yo[i] = p.obs[O * H + i];
+  }
+  for (int h = threadIdx.x; h < H; h += blockDim.x) {
+    L.a[h] = p.acc[size_t(b) * 100 + h];
+    L.st[h] = p.steer[size_t(b) * 100 + h];
+  }
+  __syncthreads();
+  const float dt = 0.15f, wb = 2.5f, rwb = 1.0f / 2.5f;
+  const float ra2 = 1.0f / kA2, rb2 = 1.0f / kB2;
+  for (int r = threadIdx.x; r < S; r += blockDim.x) {
+    float x = p.st0[0], y = p.st0[1], vx = p.st0[2], vy = p.st0[3], psi = p.st0[4];
+    float cb = 0.0f, lb = 0.0f, ub = 0.0f;
+    bool nan = false;
+    for (int h = 0; h < H; ++h) {
+      // residual of the recorded state (x_roll[:, h] = state before step h)
+      for (int o = 0; o < O; ++o) {
+        const float wc = x - L.xo[o * H + h];
+        const float ws = y - L.yo[o * H + h];
+        const float c = (-div_rc(wc * wc, kA2, ra2) - div_rc(ws * ws, kB2, rb2)) + 1.0f;
+        nan |= (c != c);
+        cb = fmaxf(cb, c);
+      }
+      const float l1 = -y + p.y_lb, u1 = y - p.y_ub;
+      nan |= (y != y);
+      lb = fmaxf(lb, l1);
+      ub = fmaxf(ub, u1);
+      if (h == H - 1) break;  // the last step's state is never recorded
+      float an, sn;
+      noisy_control(p, t, r, h, L.a[h], L.st[h], an, sn);
+      float v = sqrtf(vx * vx + vy * vy);
+      v = v + an * dt;
+      const float psidot = div_rc(v * tanf(sn), wb, rwb);
+      psi = psi + psidot * dt;
+      vx = v * cosf(psi);
+      vy = v * sinf(psi);
+      x = x + vx * dt;
+      y = y + vy * dt;
+    }
+    const float qnan = __int_as_float(0x7fc00000);
+    L.cbar[r] = nan ? qnan : cb;
+    L.lb[r] = nan ? qnan : lb;
+    L.ub[r] = nan ? qnan : ub;
+  }
+  __syncthreads();
+  ReduceScratch& rs = *L.rs;
+  float obs = 0.0f, lane = 0.0f;
+  if (p.cost == 2) {  // cvar
+    obs = block_cvar(L.cbar, S, L.list, rs);
+    const float cl = block_cvar(L.lb, S, L.list, rs);
+    const float cu = block_cvar(L.ub, S, L.list, rs);
+    lane = cl + cu;
+  } else if (p.cost == 3) {  // saa
+    obs = float(block_count_pos(L.cbar, S, rs)) / float(S);
+    const int cl = block_count_pos(L.lb, S, rs);
+    const int cu = block_count_pos(L.ub, S, rs);
+    lane = float(cl + cu) / float(S);
+  } else {  // mmd_random: beta = 1/n, sigma = 0.01 (cem.py:355-356); lane cost zeros (cem.py:427)
+    obs = block_mmd(L.cbar, nullptr, S, 0.01f, 1000.0f, rs);
+    lane = 0.0f;
+  }
+  if (threadIdx.x == 0) {
+    p.obs_cost[b] = obs;
+    p.lane_cost[b] = lane;
+  }
+}
+
+}  // namespace
+
+void launch_risk_baseline(const Params& p, int t, hipStream_t s) {
+  const size_t lds = risk_lds_bytes(p.O, p.H, p.S);
+  const int threads = p.S >= 512 ? 512 : ((p.S + 63) / 64) * 64;
+  hipLaunchKernelGGL(k_risk_baseline, dim3(p.B), dim3(threads), lds, s, p, t);
+}
+
+}  // namespace mpcmmd

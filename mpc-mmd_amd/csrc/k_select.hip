@@ -1,0 +1,268 @@
+// Stage "select": everything after the per-candidate risk, on one workgroup
+// (the batch-global argsorts make this a single-CU step):
+//
+//   argsort(res_norm) (full permutation, ellite_num_projection = B, Q6)  cem.py:233-248
+//   argsort(obs cost) over the permuted batch, top 20                   cem.py:264-289
+//   compute_cost of the 20 elites                                       cem_helper.py:232-262
+//   compute_ellite_samples (top 5)                                      cem_helper.py:264-271
+//   compute_shifted_samples (mean/cov EMA, 8x8 Cholesky, B-5 draws)     cem_helper.py:280-314
+//   per-iteration result = elite 0 of the obstacle sort (Q1)            cem.py:308-315
+//
+// Plus stage "noise": the internal Philox draws of one outer iteration.
+#include "block.hpp"
+#include "kernels.hpp"
+#include "rng.hpp"
+
+namespace mpcmmd {
+
+namespace {
+
+constexpr int kMaxSortN = 4096;
+constexpr int kN = 100;
+
+__global__ __launch_bounds__(1024) void k_select(Params p, int t) {
+  __shared__ unsigned long long keys[kMaxSortN];
+  __shared__ int perm[kMaxSortN];
+  __shared__ int el[kEliteCost];
+  __shared__ float cost20[kEliteCost];
+  __shared__ int cem5[kElite];
+  __shared__ float pe[kElite][8];
+  __shared__ double L[8][8];
+  __shared__ float mean32[8];
+  __shared__ int imin_s;
+  const int B = p.B;
+  int N = 1;
+  while (N < B) N <<= 1;
+  const int tid = threadIdx.x;
+
+  // ---- argsort(res_norm), stable ------------------------------------------
+  for (int i = tid; i < N; i += blockDim.x)
+    keys[i] = i < B ? ((unsigned long long)sort_key(p.res_norm[i]) << 32) | unsigned(i) : ~0ull;
+  bitonic_sort(keys, N);
+  for (int i = tid; i < B; i += blockDim.x) {
+    perm[i] = int(keys[i] & 0xFFFFFFFFu);
+    p.tr_proj[size_t(t) * B + i] = perm[i];
+  }
+  __syncthreads();
+  // ---- argsort(obs cost) over the permuted batch -------------------------
+  for (int i = tid; i < N; i += blockDim.x)
+    keys[i] = i < B ? ((unsigned long long)sort_key(p.obs_cost[perm[i]]) << 32) | unsigned(i) : ~0ull;
+  bitonic_sort(keys, N);
+  if (tid < kEliteCost) {
+    const int e = perm[int(keys[tid] & 0xFFFFFFFFu)];
+    el[tid] = e;
+    p.tr_obs[size_t(t) * kEliteCost + tid] = e;
+  }
+  __syncthreads();
+
+  // ---- compute_cost of the 20 elites: one wave each ----------------------
+  const int lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+  for (int j = w; j < kEliteCost; j += nw) {
+    const int e = el[j];
+    const size_t plane = size_t(B) * kN, row = size_t(e) * kN;
+    const int t0 = lane, t1 = lane + 64;
+    const bool v1 = t1 < kN;
+    const int t1c = v1 ? t1 : kN - 1;
+    auto ld = [&](int k, int tt) { return p.traj[size_t(k) * plane + row + tt]; };
+    float y[2] = {ld(1, t0), ld(1, t1c)}, xd[2] = {ld(2, t0), ld(2, t1c)}, yd[2] = {ld(3, t0), ld(3, t1c)};
+    float xdd[2] = {ld(4, t0), ld(4, t1c)}, ydd[2] = {ld(5, t0), ld(5, t1c)};
+    float st[2] = {p.steer[row + t0], p.steer[row + t1c]};
+    // neighbours for the diffs
+    const float st_d0 = __shfl_down(st[0], 1, kWave);
+    const float st_f1 = readlane_f(st[1], 0);
+    const float st_n1 = __shfl_down(st[1], 1, kWave);
+    const float st_n0 = lane < 63 ? st_d0 : st_f1;
+    const float sv[2] = {st_n0 - st[0], st_n1 - st[1]};  // valid for t < 99
+    const float sv_d0 = __shfl_down(sv[0], 1, kWave);
+    const float sv_f1 = readlane_f(sv[1], 0);
+    const float sv_n1 = __shfl_down(sv[1], 1, kWave);
+    const float sv_n0 = lane < 63 ? sv_d0 : sv_f1;
+    const float sa[2] = {sv_n0 - sv[0], sv_n1 - sv[1]};  // valid for t < 98
+    double n_des = 0, n_st = 0, n_sv = 0, n_sa = 0, n_v = 0, n_sp = 0, n_svp = 0, n_ydd = 0, n_xdd = 0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int tt = q == 0 ? t0 : t1;
+      if (tt >= kN) continue;
+      const double dd = double(y[q] - (-1.75f));
+      n_des += dd * dd;
+      n_st += double(st[q]) * double(st[q]);
+      const float v = sqrtf(xd[q] * xd[q] + yd[q] * yd[q]);
+      const double dv = double(v - p.v_des);
+      n_v += dv * dv;
+      const double sp = double(fmaxf(0.0f, fabsf(st[q]) - 0.6f));
+      n_sp += sp * sp;
+      n_ydd += double(ydd[q]) * double(ydd[q]);
+      n_xdd += double(xdd[q]) * double(xdd[q]);
+      if (tt < kN - 1) {
+        n_sv += double(sv[q]) * double(sv[q]);
+        const double svp = double(fmaxf(0.0f, fabsf(sv[q]) - 0.05f));
+        n_svp += svp * svp;
+      }
+      if (tt < kN - 2) n_sa += double(sa[q]) * double(sa[q]);
+    }
+    n_des = sqrt(wave_sum(n_des));
+    n_st = sqrt(wave_sum(n_st));
+    n_sv = sqrt(wave_sum(n_sv));
+    n_sa = sqrt(wave_sum(n_sa));
+    n_v = sqrt(wave_sum(n_v));
+    n_sp = sqrt(wave_sum(n_sp));
+    n_svp = sqrt(wave_sum(n_svp));
+    n_ydd = sqrt(wave_sum(n_ydd));
+    n_xdd = sqrt(wave_sum(n_xdd));
+    if (lane == 0) {
+      const double cobs = double(p.w_obs * p.obs_cost[e]);
+      const double clane = double(p.w_lane * p.lane_cost[e]);
+      const double tot = double(p.res_norm[e]) + 0.1 * n_v + 0.1 * (n_st + n_sv + n_sa) + 0.1 * (n_sp + n_svp) +
+                         0.02 * n_ydd + 0.02 * n_xdd + 0.0 * n_des + cobs + 0.0 * clane;
+      cost20[j] = float(tot);
+    }
+  }
+  __syncthreads();
+  // ---- top 5 by cost (stable) -------------------------------------------
+  if (tid < kEliteCost) {
+    const uint32_t kj = sort_key(cost20[tid]);
+    int r = 0;
+    for (int k = 0; k < kEliteCost; ++k) {
+      const uint32_t kk = sort_key(cost20[k]);
+      r += (kk < kj) || (kk == kj && k < tid);
+    }
+    if (r < kElite) cem5[r] = tid;
+  }
+  __syncthreads();
+  const float* pop = p.pop + size_t(t & 1) * B * 8;
+  float* pop_next = p.pop + size_t((t + 1) & 1) * B * 8;
+  if (tid < kElite * 8) {
+    const int q = tid >> 3, c = tid & 7;
+    pe[q][c] = pop[size_t(el[cem5[q]]) * 8 + c];
+  }
+  __syncthreads();
+  // ---- compute_shifted_samples (fp64) on thread 0 --------------------------
+  if (tid == 0) {
+    double c5[kElite], wgt[kElite];
+    for (int q = 0; q < kElite; ++q) c5[q] = double(cost20[cem5[q]]);
+    double cmin = c5[0];
+    for (int q = 1; q < kElite; ++q) cmin = c5[q] < cmin ? c5[q] : cmin;
+    double sw = 0.0;
+    for (int q = 0; q < kElite; ++q) {
+      wgt[q] = exp(-(1.0 / 0.9) * (c5[q] - cmin));
+      sw += wgt[q];
+    }
+    float m32[8];
+    for (int c = 0; c < 8; ++c) {
+      double s = 0.0;
+      for (int q = 0; q < kElite; ++q) s += wgt[q] * double(pe[q][c]);
+      m32[c] = float((1.0 - 0.6) * double(p.mean[c]) + 0.6 * s / sw);
+      mean32[c] = m32[c];
+    }
+    double cv[8][8];
+    for (int a = 0; a < 8; ++a)
+      for (int c = 0; c < 8; ++c) {
+        double s = 0.0;
+        for (int q = 0; q < kElite; ++q)
+          s += wgt[q] * (double(pe[q][a]) - double(m32[a])) * (double(pe[q][c]) - double(m32[c]));
+        const float v = float((1.0 - 0.6) * double(p.cov[a * 8 + c]) + 0.6 * s / sw + (a == c ? 0.01 : 0.0));
+        cv[a][c] = double(v);
+        p.cov[a * 8 + c] = v;
+      }
+    for (int c = 0; c < 8; ++c) p.mean[c] = m32[c];
+    // Cholesky (lower) of the fp32 covariance, in fp64
+    for (int j = 0; j < 8; ++j) {
+      double d = cv[j][j];
+      for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k];
+      d = sqrt(d);
+      L[j][j] = d;
+      for (int i = j + 1; i < 8; ++i) {
+        double s = cv[i][j];
+        for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k];
+        L[i][j] = s / d;
+      }
+      for (int i = 0; i < j; ++i) L[i][j] = 0.0;
+    }
+    // idx_min = argmin(cost_batch_temp) (== 0 unless NaN; jnp.argmin: first NaN)
+    int im = 0;
+    for (int q = 0; q < kElite; ++q)
+      if (c5[q] != c5[q]) {
+        im = q;
+        break;
+      }
+    imin_s = im;
+    for (int q = 0; q < kElite; ++q) p.tr_cem[size_t(t) * kElite + q] = cem5[q];
+  }
+  __syncthreads();
+  // ---- new population: [elites; mean + L z], v columns clipped -----------
+  const float* z = p.resample + size_t(t) * (B - kElite) * 8;
+  for (int i = tid; i < B; i += blockDim.x) {
+    float row[8];
+    if (i < kElite) {
+      for (int c = 0; c < 8; ++c) row[c] = pe[i][c];
+    } else {
+      const float* zi = z + size_t(i - kElite) * 8;
+      for (int a = 0; a < 8; ++a) {
+        double s = double(mean32[a]);
+        for (int c = 0; c <= a; ++c) s += L[a][c] * double(zi[c]);
+        row[a] = float(s);
+      }
+      for (int c = 0; c < 4; ++c) row[c] = fminf(fmaxf(row[c], 0.1f), 30.0f);
+    }
+    for (int c = 0; c < 8; ++c) pop_next[size_t(i) * 8 + c] = row[c];
+  }
+  // ---- per-iteration result (cem.py:314-315) ------------------------------
+  if (tid < kResultStride) {
+    const int e = el[imin_s];
+    float* r = p.results + size_t(t) * kResultStride;
+    float v = 0.0f;
+    if (tid < 11) v = p.cx[size_t(e) * 11 + tid];
+    else if (tid < 22) v = p.cy[size_t(e) * 11 + tid - 11];
+    else if (tid == 22) v = p.lane_cost[e];
+    else if (tid == 23) v = p.obs_cost[e];
+    else if (tid == 24) v = p.cost == 0 ? p.sigma[e] : 0.0f;
+    else if (tid < 45) v = p.cost == 0 ? p.res_beta[size_t(e) * kBetaIters + tid - 25] : 0.0f;
+    else if (tid - 45 < p.n) v = p.cost == 0 ? p.beta[size_t(e) * p.n + tid - 45] : 0.0f;
+    r[tid] = v;
+  }
+}
+
+// internal draws of outer iteration t: roll [3][H][S] and resample [B-5][8]
+__global__ __launch_bounds__(256) void k_noise(Params p, int t) {
+  const int S = p.S, H = p.H;
+  const uint32_t k0 = iteration_key0(p.idx_mpc, t), k1 = p.seed;
+  const int nroll = (S * H + 3) / 4;
+  const int nres = ((p.B - kElite) * 8 + 3) / 4;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  float* roll = const_cast<float*>(p.roll) + size_t(t) * 3 * H * S;
+  float* res = const_cast<float*>(p.resample) + size_t(t) * (p.B - kElite) * 8;
+  if (j < 3 * nroll) {
+    const int st = j / nroll, jb = j % nroll;
+    double z[4];
+    philox_normals4(k0, k1, kStreamRollAcc + st, 0u, uint32_t(jb), z);
+    for (int q = 0; q < 4; ++q) {
+      const int e = 4 * jb + q;
+      if (e >= S * H) break;
+      const int s = e / H, h = e % H;
+      roll[(size_t(st) * H + h) * S + s] = float(z[q]);
+    }
+  } else if (j < 3 * nroll + nres) {
+    const int jb = j - 3 * nroll;
+    double z[4];
+    philox_normals4(k0, k1, kStreamResample, 0u, uint32_t(jb), z);
+    for (int q = 0; q < 4; ++q) {
+      const int e = 4 * jb + q;
+      if (e < (p.B - kElite) * 8) res[e] = float(z[q]);
+    }
+  }
+}
+
+}  // namespace
+
+void launch_select(const Params& p, int t, hipStream_t s) {
+  hipLaunchKernelGGL(k_select, dim3(1), dim3(1024), 0, s, p, t);
+}
+
+void launch_noise(const Params& p, int t, hipStream_t s) {
+  const int nroll = (p.S * p.H + 3) / 4;
+  const int nres = ((p.B - kElite) * 8 + 3) / 4;
+  const int total = 3 * nroll + nres;
+  hipLaunchKernelGGL(k_noise, dim3((total + 255) / 256), dim3(256), 0, s, p, t);
+}
+
+}  // namespace mpcmmd

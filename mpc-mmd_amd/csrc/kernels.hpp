@@ -1,0 +1,74 @@
+// Kernel argument block and launch declarations.  One struct for every
+// kernel keeps the host side simple: it is passed by value (kernarg segment).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mpcmmd {
+
+constexpr int kMaxH = 100;
+constexpr int kMaxReduced = 32;        // n for mmd_opt (M = n^2 <= 1024) -- see DESIGN.md
+constexpr int kBetaSamples = 100;      // compute_beta.py:14
+constexpr int kBetaIters = 20;         // compute_beta.py:15
+constexpr int kBetaElite = 11;         // compute_beta.py:26
+constexpr int kEliteCost = 20;         // cem.py:140
+constexpr int kElite = 5;              // cem.py:138
+constexpr int kResultStride = 11 + 11 + 2 + 1 + 20 + kMaxReduced;  // cx, cy, lane, obs, sigma, res_beta, beta
+
+struct Params {
+  // shapes / configuration
+  int32_t B, S, H, O, n, M, T;
+  int32_t cost;      // MPCMMD_COST_*
+  int32_t noise;     // MPCMMD_NOISE_*
+  int32_t idx_mpc;
+  uint32_t seed;
+  float sigma_acc, sigma_steer, acc_const, steer_const, K_steer;
+  float y_lb, y_ub, v_des;
+  float w_obs, w_lane;
+  // constants (device)
+  const float* basis;      // [3][100][11] fp32: P, Pd, Pdd
+  const double* guess_g;   // [2][11][4]  (x: v-columns, y: y-columns)
+  const double* proj_m;    // [2][11][11] (Kinv[:11,:11] for x, y)
+  const double* fit;       // [11][H]
+  const double* solve_c;   // [4][11] per solve: guess h_x, h_y, proj e_x, e_y
+  const float* obs;        // [2][O][H] x_obs, y_obs (first H columns)
+  const float* st0;        // [5] initial rollout state
+  // noise tables, device layout (iteration-major, sample-minor for coalescing)
+  const float* roll;       // [T][3][H][S]
+  const float* resample;   // [T][B-5][8]
+  const float* beta_z0;    // [100][M+1]
+  const float* beta_z;     // [20][89][M+1]
+  // carry / state
+  float* pop;              // [2][B][8] double-buffered population
+  float* mean;             // [8]
+  float* cov;              // [64]
+  float* lam_x;            // [B][11]
+  float* lam_y;            // [B][11]
+  float* s_lane;           // [B][198]
+  // per-iteration intermediates
+  float* cx;               // [B][11]
+  float* cy;               // [B][11]
+  float* traj;             // [6][B][100]: x, y, xd, yd, xdd, ydd
+  float* res_norm;         // [B]
+  float* acc;              // [B][100]
+  float* steer;            // [B][100]
+  float* obs_cost;         // [B]
+  float* lane_cost;        // [B]
+  float* beta;             // [B][n]
+  float* sigma;            // [B]
+  float* res_beta;         // [B][20]
+  // outputs
+  float* results;          // [T][kResultStride]
+  int32_t* tr_proj;        // [T][B]
+  int32_t* tr_obs;         // [T][20]
+  int32_t* tr_cem;         // [T][5]
+};
+
+void launch_noise(const Params& p, int t, hipStream_t s);
+void launch_front(const Params& p, int t, hipStream_t s);
+void launch_risk(const Params& p, int t, hipStream_t s);
+void launch_select(const Params& p, int t, hipStream_t s);
+void launch_init_pop(const Params& p, hipStream_t s);
+void launch_fill_fixed(const Params& p, hipStream_t s);
+
+}  // namespace mpcmmd

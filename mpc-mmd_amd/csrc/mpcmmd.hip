@@ -1,0 +1,647 @@
+// libmpcmmd: the C ABI (include/mpcmmd.h), handle / buffer management and
+// the per-iteration launch sequence.  Host code is plain HIP runtime; no
+// torch, no allocation after mpcmmd_create.
+#include "../../include/mpcmmd.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "host_constants.hpp"
+#include "kernels.hpp"
+#include "rng.hpp"
+
+namespace mpcmmd {
+void launch_risk_baseline(const Params& p, int t, hipStream_t s);
+void launch_risk_mmdopt(const Params& p, int t, hipStream_t s);
+size_t mmdopt_lds_bytes(const Params& p);
+}  // namespace mpcmmd
+
+using namespace mpcmmd;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define HIPC(x)                                                                                     \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess)                                                                           \
+      throw HipError(std::string(#x) + ": " + hipGetErrorString(e_) + " (" + __FILE__ + ":" +     \
+                     std::to_string(__LINE__) + ")");                                              \
+  } while (0)
+
+enum KernelId { kKNoise = 0, kKFront, kKRiskBaseline, kKRiskMmdOpt, kKSelect, kNumKernels };
+const char* kKernelNames[kNumKernels] = {"noise", "front", "risk_baseline", "risk_mmdopt", "select"};
+
+}  // namespace
+
+struct mpcmmd_handle {
+  mpcmmd_config cfg{};
+  ProblemConsts pc;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  Params p{};
+  int B = 0, S = 0, H = 0, O = 0, n = 0, M = 0, T = 0;
+  std::map<std::string, std::pair<void*, size_t>> bufs;
+  // solve state
+  int cost = -1;
+  bool begun = false;
+  int last_t = -1;
+  bool ext_roll = false, ext_res = false;
+  bool beta_tables_internal = false;  // device beta tables hold the internal streams
+  // profiling
+  bool prof = false;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+  std::vector<hipEvent_t> free_events;
+  int launches[kNumKernels] = {0};
+  double total_ms[kNumKernels] = {0};
+
+  void* alloc(const std::string& name, size_t bytes) {
+    void* d = nullptr;
+    if (bytes == 0) bytes = 16;
+    HIPC(hipMalloc(&d, bytes));
+    HIPC(hipMemset(d, 0, bytes));
+    bufs[name] = {d, bytes};
+    return d;
+  }
+  hipEvent_t ev() {
+    if (!free_events.empty()) {
+      hipEvent_t e = free_events.back();
+      free_events.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    HIPC(hipEventCreate(&e));
+    return e;
+  }
+  template <class F>
+  void launch(int kid, F&& f) {
+    if (!prof) {
+      f();
+      HIPC(hipGetLastError());
+      return;
+    }
+    hipEvent_t a = ev(), b = ev();
+    HIPC(hipEventRecord(a, stream));
+    f();
+    HIPC(hipGetLastError());
+    HIPC(hipEventRecord(b, stream));
+    pending.push_back({kid, {a, b}});
+  }
+  void collect() {
+    for (auto& pe : pending) {
+      float ms = 0.f;
+      HIPC(hipEventSynchronize(pe.second.second));
+      HIPC(hipEventElapsedTime(&ms, pe.second.first, pe.second.second));
+      launches[pe.first] += 1;
+      total_ms[pe.first] += ms;
+      free_events.push_back(pe.second.first);
+      free_events.push_back(pe.second.second);
+    }
+    pending.clear();
+  }
+};
+
+namespace {
+
+void check_device(mpcmmd_handle* h) { HIPC(hipSetDevice(h->device)); }
+
+// host Philox normals of stream (stream, word1) with key (k0, k1): `count` values
+std::vector<float> host_normals(uint32_t k0, uint32_t k1, uint32_t stream, uint32_t word1, size_t count) {
+  std::vector<float> out(count);
+  double z[4];
+  for (size_t j = 0; j * 4 < count; ++j) {
+    philox_normals4(k0, k1, stream, word1, uint32_t(j), z);
+    for (int q = 0; q < 4 && j * 4 + q < count; ++q) out[j * 4 + q] = float(z[q]);
+  }
+  return out;
+}
+
+bool chol8(const double* a, double* L) {
+  for (int i = 0; i < 64; ++i) L[i] = 0.0;
+  for (int j = 0; j < 8; ++j) {
+    double d = a[j * 8 + j];
+    for (int k = 0; k < j; ++k) d -= L[j * 8 + k] * L[j * 8 + k];
+    if (!(d > 0.0)) return false;
+    d = std::sqrt(d);
+    L[j * 8 + j] = d;
+    for (int i = j + 1; i < 8; ++i) {
+      double s = a[i * 8 + j];
+      for (int k = 0; k < j; ++k) s -= L[i * 8 + k] * L[j * 8 + k];
+      L[i * 8 + j] = s / d;
+    }
+  }
+  return true;
+}
+
+void upload(mpcmmd_handle* h, const char* name, const void* src, size_t bytes, size_t offset = 0) {
+  auto it = h->bufs.find(name);
+  if (it == h->bufs.end() || offset + bytes > it->second.second) throw std::runtime_error(std::string("buffer ") + name);
+  HIPC(hipMemcpyAsync(static_cast<char*>(it->second.first) + offset, src, bytes, hipMemcpyHostToDevice, h->stream));
+}
+
+void gen_beta_tables(mpcmmd_handle* h) {
+  const int M1 = h->M + 1;
+  const uint32_t k0 = kFixedKey0, k1 = h->cfg.seed;
+  auto z0 = host_normals(k0, k1, kStreamBetaZ0, 0, size_t(kBetaSamples) * M1);
+  upload(h, "beta_z0", z0.data(), z0.size() * 4);
+  const size_t per = size_t(kBetaSamples - kBetaElite) * M1;
+  for (int t = 0; t < kBetaIters; ++t) {
+    auto z = host_normals(k0, k1, kStreamBetaZ, uint32_t(t), per);
+    upload(h, "beta_z", z.data(), per * 4, size_t(t) * per * 4);
+  }
+  HIPC(hipStreamSynchronize(h->stream));
+  h->beta_tables_internal = true;
+}
+
+void run_stage(mpcmmd_handle* h, int stage, int t) {
+  const Params& p = h->p;
+  switch (stage) {
+    case 0:
+      h->launch(kKNoise, [&] { launch_noise(p, t, h->stream); });
+      break;
+    case 1:
+      h->launch(kKFront, [&] { launch_front(p, t, h->stream); });
+      break;
+    case 2:
+      if (p.cost == MPCMMD_COST_MMD_OPT)
+        h->launch(kKRiskMmdOpt, [&] { launch_risk_mmdopt(p, t, h->stream); });
+      else
+        h->launch(kKRiskBaseline, [&] { launch_risk_baseline(p, t, h->stream); });
+      break;
+    case 3:
+      h->launch(kKSelect, [&] { launch_select(p, t, h->stream); });
+      break;
+    default:
+      throw std::invalid_argument("stage must be 0..3");
+  }
+}
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const HipError& e) {
+    return fail(MPCMMD_E_HIP, e.what());
+  } catch (const std::invalid_argument& e) {
+    return fail(MPCMMD_E_INVALID, e.what());
+  } catch (const std::exception& e) {
+    return fail(MPCMMD_E_INVALID, e.what());
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t mpcmmd_abi_version(void) { return MPCMMD_ABI_VERSION; }
+const char* mpcmmd_last_error(void) { return g_err.c_str(); }
+
+int32_t mpcmmd_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
+  if (!cfg || !out) return fail(MPCMMD_E_INVALID, "null argument");
+  *out = nullptr;
+  const mpcmmd_config& c = *cfg;
+  if (c.num_reduced < 2 || c.num_obs < 1 || c.num_prime < 2 || c.num_prime > 100 || c.num_batch < 20 ||
+      c.num_batch > 4096 || c.maxiter_cem < 1 || (c.noise != 0 && c.noise != 1) ||
+      (c.variant != 0 && c.variant != 1))
+    return fail(MPCMMD_E_INVALID,
+                "config out of range (num_reduced>=2, num_obs>=1, 2<=num_prime<=100, 20<=num_batch<=4096)");
+  if (c.num_reduced > 1024) return fail(MPCMMD_E_UNSUPPORTED, "num_reduced > 1024");
+  if (size_t(c.num_obs) * c.num_prime > 8192) return fail(MPCMMD_E_UNSUPPORTED, "num_obs * num_prime > 8192");
+  auto* h = new mpcmmd_handle();
+  int rc = guarded([&] {
+    h->cfg = c;
+    h->device = c.device;
+    int ndev = 0;
+    HIPC(hipGetDeviceCount(&ndev));
+    if (c.device < 0 || c.device >= ndev) throw std::invalid_argument("device ordinal out of range");
+    HIPC(hipSetDevice(c.device));
+    HIPC(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    h->own_stream = true;
+    h->pc = build_constants(c.num_prime, c.variant);
+    h->B = c.num_batch;
+    h->S = c.num_reduced;
+    h->H = c.num_prime;
+    h->O = c.num_obs;
+    h->n = c.num_reduced;
+    h->M = c.num_reduced * c.num_reduced;
+    h->T = c.maxiter_cem;
+    const int B = h->B, S = h->S, H = h->H, O = h->O, T = h->T;
+    const bool mmd_ok = h->n <= kMaxReduced;
+    Params& p = h->p;
+    p.B = B;
+    p.S = S;
+    p.H = H;
+    p.O = O;
+    p.n = h->n;
+    p.M = h->M;
+    p.T = T;
+    p.noise = c.noise;
+    p.seed = c.seed;
+    p.sigma_acc = c.noise_level;
+    p.sigma_steer = c.noise_level;
+    p.acc_const = c.acc_const_noise;
+    p.steer_const = c.steer_const_noise;
+    // beta noise: steer_pert = float32(K_steer * sigma_steer) * (2 b - 1) (cem_helper.py:436)
+    p.K_steer = float(h->pc.K_steer * double(c.noise_level));
+    p.y_lb = float(h->pc.y_lb);
+    p.y_ub = float(h->pc.y_ub);
+    // constants
+    std::vector<float> basis(3 * kNum * kNvar);
+    for (int i = 0; i < kNum * kNvar; ++i) {
+      basis[i] = float(h->pc.P[i]);
+      basis[kNum * kNvar + i] = float(h->pc.Pd[i]);
+      basis[2 * kNum * kNvar + i] = float(h->pc.Pdd[i]);
+    }
+    p.basis = (const float*)h->alloc("basis", basis.size() * 4);
+    // guess: c_bar = G v + h with G[k][j] = sum_i Kinv[k][i] (-k_p colsum_j[i])
+    std::vector<double> gg(2 * kNvar * 4);
+    for (int xy = 0; xy < 2; ++xy) {
+      const auto& Ki = xy == 0 ? h->pc.guess_kinv_x : h->pc.guess_kinv_y;
+      const auto& cs = xy == 0 ? h->pc.guess_colsum_x : h->pc.guess_colsum_y;
+      const int n = xy == 0 ? 14 : 15;
+      const double kp = xy == 0 ? h->pc.k_p_v : h->pc.k_p;
+      for (int k = 0; k < kNvar; ++k)
+        for (int j = 0; j < 4; ++j) {
+          double s = 0.0;
+          for (int i = 0; i < kNvar; ++i) s += Ki[k * n + i] * (-kp * cs[j * kNvar + i]);
+          gg[(xy * kNvar + k) * 4 + j] = s;
+        }
+    }
+    p.guess_g = (const double*)h->alloc("guess_g", gg.size() * 8);
+    std::vector<double> pm(2 * kNvar * kNvar);
+    for (int xy = 0; xy < 2; ++xy) {
+      const auto& Ki = xy == 0 ? h->pc.proj_kinv_x : h->pc.proj_kinv_y;
+      const int n = xy == 0 ? 14 : 15;
+      for (int k = 0; k < kNvar; ++k)
+        for (int j = 0; j < kNvar; ++j) pm[(xy * kNvar + k) * kNvar + j] = Ki[k * n + j];
+    }
+    p.proj_m = (const double*)h->alloc("proj_m", pm.size() * 8);
+    p.fit = (const double*)h->alloc("fit", h->pc.fit.size() * 8);
+    p.solve_c = (const double*)h->alloc("solve_c", 4 * kNvar * 8);
+    p.obs = (const float*)h->alloc("obs", size_t(2) * O * H * 4);
+    p.st0 = (const float*)h->alloc("st0", 8 * 4);
+    p.roll = (const float*)h->alloc("roll", size_t(T) * 3 * H * S * 4);
+    p.resample = (const float*)h->alloc("resample", size_t(T) * (B - kElite) * 8 * 4);
+    if (mmd_ok) {
+      p.beta_z0 = (const float*)h->alloc("beta_z0", size_t(kBetaSamples) * (h->M + 1) * 4);
+      p.beta_z = (const float*)h->alloc("beta_z", size_t(kBetaIters) * (kBetaSamples - kBetaElite) * (h->M + 1) * 4);
+    }
+    p.pop = (float*)h->alloc("pop", size_t(2) * B * 8 * 4);
+    p.mean = (float*)h->alloc("mean", 8 * 4);
+    p.cov = (float*)h->alloc("cov", 64 * 4);
+    p.lam_x = (float*)h->alloc("lam_x", size_t(B) * kNvar * 4);
+    p.lam_y = (float*)h->alloc("lam_y", size_t(B) * kNvar * 4);
+    p.s_lane = (float*)h->alloc("s_lane", size_t(B) * kLane * 4);
+    p.cx = (float*)h->alloc("cx", size_t(B) * kNvar * 4);
+    p.cy = (float*)h->alloc("cy", size_t(B) * kNvar * 4);
+    p.traj = (float*)h->alloc("traj", size_t(6) * B * kNum * 4);
+    p.res_norm = (float*)h->alloc("res_norm", size_t(B) * 4);
+    p.acc = (float*)h->alloc("acc", size_t(B) * kNum * 4);
+    p.steer = (float*)h->alloc("steer", size_t(B) * kNum * 4);
+    p.obs_cost = (float*)h->alloc("obs_cost", size_t(B) * 4);
+    p.lane_cost = (float*)h->alloc("lane_cost", size_t(B) * 4);
+    p.beta = (float*)h->alloc("beta", size_t(B) * h->n * 4);
+    p.sigma = (float*)h->alloc("sigma", size_t(B) * 4);
+    p.res_beta = (float*)h->alloc("res_beta", size_t(B) * kBetaIters * 4);
+    p.results = (float*)h->alloc("results", size_t(T) * kResultStride * 4);
+    p.tr_proj = (int32_t*)h->alloc("tr_proj", size_t(T) * B * 4);
+    p.tr_obs = (int32_t*)h->alloc("tr_obs", size_t(T) * kEliteCost * 4);
+    p.tr_cem = (int32_t*)h->alloc("tr_cem", size_t(T) * kElite * 4);
+    upload(h, "basis", basis.data(), basis.size() * 4);
+    upload(h, "guess_g", gg.data(), gg.size() * 8);
+    upload(h, "proj_m", pm.data(), pm.size() * 8);
+    upload(h, "fit", h->pc.fit.data(), h->pc.fit.size() * 8);
+    HIPC(hipStreamSynchronize(h->stream));
+    return MPCMMD_OK;
+  });
+  if (rc != MPCMMD_OK) {
+    mpcmmd_destroy(h);
+    return rc;
+  }
+  *out = h;
+  return MPCMMD_OK;
+}
+
+void mpcmmd_destroy(mpcmmd_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (auto& kv : h->bufs) (void)hipFree(kv.second.first);
+  for (auto& pe : h->pending) {
+    (void)hipEventDestroy(pe.second.first);
+    (void)hipEventDestroy(pe.second.second);
+  }
+  for (auto e : h->free_events) (void)hipEventDestroy(e);
+  if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+int mpcmmd_set_stream(mpcmmd_handle* h, void* s) {
+  if (!h) return fail(MPCMMD_E_INVALID, "null handle");
+  return guarded([&] {
+    check_device(h);
+    HIPC(hipStreamSynchronize(h->stream));
+    if (h->own_stream) HIPC(hipStreamDestroy(h->stream));
+    h->own_stream = false;
+    h->stream = static_cast<hipStream_t>(s);
+    return MPCMMD_OK;
+  });
+}
+
+void* mpcmmd_get_stream(mpcmmd_handle* h) { return h ? (void*)h->stream : nullptr; }
+
+int mpcmmd_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const float init_state[6],
+                 const float mean[8], const float cov[64], const float* x_obs, const float* y_obs, float v_des,
+                 const mpcmmd_draws* draws) {
+  if (!h || !init_state || !mean || !cov || !x_obs || !y_obs) return fail(MPCMMD_E_INVALID, "null argument");
+  if (cost_kind < 0 || cost_kind > 3) return fail(MPCMMD_E_INVALID, "cost_kind must be 0..3");
+  if (cost_kind == MPCMMD_COST_MMD_OPT && h->n > kMaxReduced)
+    return fail(MPCMMD_E_UNSUPPORTED, "mmd_opt needs num_reduced <= 32 (M = n^2 <= 1024)");
+  return guarded([&] {
+    check_device(h);
+    Params& p = h->p;
+    const int B = h->B, S = h->S, H = h->H, O = h->O, T = h->T;
+    h->cost = cost_kind;
+    p.cost = cost_kind;
+    p.idx_mpc = idx_mpc;
+    p.v_des = v_des;
+    // cem.py:161-163 weights (obs, lane)
+    const float w_obs[4] = {1e3f, 1e3f, 1e3f, 1e6f}, w_lane[4] = {0.f, 0.f, 0.f, 1e6f};
+    p.w_obs = w_obs[cost_kind];
+    p.w_lane = w_lane[cost_kind];
+    // boundary vectors (cem_helper.py:152-167) and the per-solve KKT columns
+    const double bx[3] = {init_state[0], init_state[2], init_state[4]};
+    const double by[4] = {init_state[1], init_state[3], init_state[5], 0.0};
+    std::vector<double> sc(4 * kNvar, 0.0);
+    for (int k = 0; k < kNvar; ++k) {
+      for (int e = 0; e < 3; ++e) sc[0 * kNvar + k] += h->pc.guess_kinv_x[k * 14 + kNvar + e] * bx[e];
+      for (int e = 0; e < 4; ++e) sc[1 * kNvar + k] += h->pc.guess_kinv_y[k * 15 + kNvar + e] * by[e];
+      for (int e = 0; e < 3; ++e) sc[2 * kNvar + k] += h->pc.proj_kinv_x[k * 14 + kNvar + e] * bx[e];
+      for (int e = 0; e < 4; ++e) sc[3 * kNvar + k] += h->pc.proj_kinv_y[k * 15 + kNvar + e] * by[e];
+    }
+    upload(h, "solve_c", sc.data(), sc.size() * 8);
+    float st0[8] = {init_state[0], init_state[1], init_state[2], init_state[3],
+                    atan2f(init_state[3], init_state[2]), 0.f, 0.f, 0.f};
+    upload(h, "st0", st0, sizeof(st0));
+    std::vector<float> ob(size_t(2) * O * H);
+    for (int o = 0; o < O; ++o)
+      for (int t = 0; t < H; ++t) {
+        ob[size_t(o) * H + t] = x_obs[o * kNum + t];
+        ob[size_t(O) * H + o * H + t] = y_obs[o * kNum + t];
+      }
+    upload(h, "obs", ob.data(), ob.size() * 4);
+    // sampling_param (cem_helper.py:122-150): fixed key
+    std::vector<float> z0;
+    if (draws && draws->pop0) z0.assign(draws->pop0, draws->pop0 + size_t(B) * 8);
+    else z0 = host_normals(kFixedKey0, h->cfg.seed, kStreamPop0, 0, size_t(B) * 8);
+    double cv[64], L[64];
+    for (int i = 0; i < 64; ++i) cv[i] = double(cov[i]);
+    if (!chol8(cv, L)) throw std::invalid_argument("cov_param_init is not positive definite");
+    std::vector<float> pop(size_t(B) * 8);
+    for (int b = 0; b < B; ++b)
+      for (int a = 0; a < 8; ++a) {
+        double s = double(mean[a]);
+        for (int c = 0; c <= a; ++c) s += L[a * 8 + c] * double(z0[size_t(b) * 8 + c]);
+        float v = float(s);
+        if (a < 4) v = fminf(fmaxf(v, 0.1f), 30.0f);
+        pop[size_t(b) * 8 + a] = v;
+      }
+    upload(h, "pop", pop.data(), pop.size() * 4);
+    upload(h, "mean", mean, 8 * 4);
+    upload(h, "cov", cov, 64 * 4);
+    HIPC(hipMemsetAsync(p.lam_x, 0, size_t(B) * kNvar * 4, h->stream));
+    HIPC(hipMemsetAsync(p.lam_y, 0, size_t(B) * kNvar * 4, h->stream));
+    HIPC(hipMemsetAsync(p.s_lane, 0, size_t(B) * kLane * 4, h->stream));
+    // external noise rows: [T][3][S][H] -> device [T][3][H][S]
+    h->ext_roll = draws && draws->roll;
+    h->ext_res = draws && draws->resample;
+    if (h->ext_roll) {
+      std::vector<float> r(size_t(T) * 3 * H * S);
+      for (int t = 0; t < T; ++t)
+        for (int k = 0; k < 3; ++k)
+          for (int s = 0; s < S; ++s)
+            for (int q = 0; q < H; ++q)
+              r[((size_t(t) * 3 + k) * H + q) * S + s] = draws->roll[((size_t(t) * 3 + k) * S + s) * H + q];
+      upload(h, "roll", r.data(), r.size() * 4);
+    }
+    if (h->ext_res) upload(h, "resample", draws->resample, size_t(T) * (B - kElite) * 8 * 4);
+    if (cost_kind == MPCMMD_COST_MMD_OPT) {
+      const size_t M1 = size_t(h->M) + 1;
+      const bool ext_b = draws && (draws->beta_z0 || draws->beta_z);
+      if (ext_b) {
+        if (!draws->beta_z0 || !draws->beta_z) throw std::invalid_argument("beta_z0 and beta_z go together");
+        upload(h, "beta_z0", draws->beta_z0, size_t(kBetaSamples) * M1 * 4);
+        upload(h, "beta_z", draws->beta_z, size_t(kBetaIters) * (kBetaSamples - kBetaElite) * M1 * 4);
+        h->beta_tables_internal = false;
+      } else if (!h->beta_tables_internal) {
+        gen_beta_tables(h);
+      }
+    }
+    h->begun = true;
+    h->last_t = -1;
+    return MPCMMD_OK;
+  });
+}
+
+int mpcmmd_iterate(mpcmmd_handle* h, int32_t t_begin, int32_t count) {
+  if (!h) return fail(MPCMMD_E_INVALID, "null handle");
+  if (!h->begun) return fail(MPCMMD_E_STATE, "mpcmmd_iterate before mpcmmd_begin");
+  if (t_begin < 0 || count < 0 || t_begin + count > h->T) return fail(MPCMMD_E_INVALID, "iteration range");
+  return guarded([&] {
+    check_device(h);
+    for (int t = t_begin; t < t_begin + count; ++t) {
+      if (!h->ext_roll || !h->ext_res) {
+        if (h->ext_roll != h->ext_res) throw std::invalid_argument("roll and resample draws go together");
+        run_stage(h, 0, t);
+      }
+      run_stage(h, 1, t);
+      run_stage(h, 2, t);
+      run_stage(h, 3, t);
+      h->last_t = t;
+    }
+    return MPCMMD_OK;
+  });
+}
+
+int mpcmmd_sync(mpcmmd_handle* h) {
+  if (!h) return fail(MPCMMD_E_INVALID, "null handle");
+  return guarded([&] {
+    check_device(h);
+    HIPC(hipStreamSynchronize(h->stream));
+    if (h->prof) h->collect();
+    return MPCMMD_OK;
+  });
+}
+
+int mpcmmd_finish(mpcmmd_handle* h, mpcmmd_result* out) {
+  if (!h || !out) return fail(MPCMMD_E_INVALID, "null argument");
+  if (!h->begun || h->last_t < 0) return fail(MPCMMD_E_STATE, "no iteration has run");
+  return guarded([&] {
+    check_device(h);
+    HIPC(hipStreamSynchronize(h->stream));
+    if (h->prof) h->collect();
+    std::vector<float> r(kResultStride);
+    HIPC(hipMemcpy(r.data(), h->p.results + size_t(h->last_t) * kResultStride, kResultStride * 4,
+                   hipMemcpyDeviceToHost));
+    std::memcpy(out->cx, &r[0], 11 * 4);
+    std::memcpy(out->cy, &r[11], 11 * 4);
+    out->cost_lane = r[22];
+    out->cost_obs = r[23];
+    out->sigma = r[24];
+    std::memcpy(out->res_beta, &r[25], 20 * 4);
+    if (out->beta && h->cost == MPCMMD_COST_MMD_OPT) std::memcpy(out->beta, &r[45], size_t(h->n) * 4);
+    const int T = h->last_t + 1;
+    if (out->elite_proj)
+      HIPC(hipMemcpy(out->elite_proj, h->p.tr_proj, size_t(T) * h->B * 4, hipMemcpyDeviceToHost));
+    if (out->elite_obs)
+      HIPC(hipMemcpy(out->elite_obs, h->p.tr_obs, size_t(T) * kEliteCost * 4, hipMemcpyDeviceToHost));
+    if (out->elite_cem)
+      HIPC(hipMemcpy(out->elite_cem, h->p.tr_cem, size_t(T) * kElite * 4, hipMemcpyDeviceToHost));
+    return MPCMMD_OK;
+  });
+}
+
+int mpcmmd_solve(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const float init_state[6],
+                 const float mean[8], const float cov[64], const float* x_obs, const float* y_obs, float v_des,
+                 const mpcmmd_draws* draws, mpcmmd_result* out) {
+  int rc = mpcmmd_begin(h, cost_kind, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des, draws);
+  if (rc) return rc;
+  rc = mpcmmd_iterate(h, 0, h->T);
+  if (rc) return rc;
+  return mpcmmd_finish(h, out);
+}
+
+int mpcmmd_profile(mpcmmd_handle* h, int32_t enable) {
+  if (!h) return fail(MPCMMD_E_INVALID, "null handle");
+  return guarded([&] {
+    check_device(h);
+    HIPC(hipStreamSynchronize(h->stream));
+    h->collect();
+    h->prof = enable != 0;
+    for (int k = 0; k < kNumKernels; ++k) {
+      h->launches[k] = 0;
+      h->total_ms[k] = 0.0;
+    }
+    return MPCMMD_OK;
+  });
+}
+
+int mpcmmd_kernel_times(mpcmmd_handle* h, int32_t* launches, double* total_ms, int32_t max_kernels) {
+  if (!h) return fail(MPCMMD_E_INVALID, "null handle");
+  return guarded([&] {
+    check_device(h);
+    h->collect();
+    for (int k = 0; k < kNumKernels && k < max_kernels; ++k) {
+      if (launches) launches[k] = h->launches[k];
+      if (total_ms) total_ms[k] = h->total_ms[k];
+    }
+    return int(kNumKernels);
+  });
+}
+
+const char* mpcmmd_kernel_name(int32_t id) {
+  return (id >= 0 && id < kNumKernels) ? kKernelNames[id] : nullptr;
+}
+
+int mpcmmd_buffer_info(mpcmmd_handle* h, const char* name, size_t* bytes) {
+  if (!h || !name) return fail(MPCMMD_E_INVALID, "null argument");
+  auto it = h->bufs.find(name);
+  if (it == h->bufs.end()) return fail(MPCMMD_E_INVALID, std::string("no buffer ") + name);
+  if (bytes) *bytes = it->second.second;
+  return MPCMMD_OK;
+}
+
+int mpcmmd_read(mpcmmd_handle* h, const char* name, void* dst, size_t bytes) {
+  if (!h || !name || !dst) return fail(MPCMMD_E_INVALID, "null argument");
+  auto it = h->bufs.find(name);
+  if (it == h->bufs.end()) return fail(MPCMMD_E_INVALID, std::string("no buffer ") + name);
+  if (bytes > it->second.second) return fail(MPCMMD_E_INVALID, "read larger than buffer");
+  return guarded([&] {
+    check_device(h);
+    HIPC(hipStreamSynchronize(h->stream));
+    HIPC(hipMemcpy(dst, it->second.first, bytes, hipMemcpyDeviceToHost));
+    return MPCMMD_OK;
+  });
+}
+
+int mpcmmd_write(mpcmmd_handle* h, const char* name, const void* src, size_t bytes) {
+  if (!h || !name || !src) return fail(MPCMMD_E_INVALID, "null argument");
+  auto it = h->bufs.find(name);
+  if (it == h->bufs.end()) return fail(MPCMMD_E_INVALID, std::string("no buffer ") + name);
+  if (bytes > it->second.second) return fail(MPCMMD_E_INVALID, "write larger than buffer");
+  return guarded([&] {
+    check_device(h);
+    HIPC(hipStreamSynchronize(h->stream));
+    HIPC(hipMemcpy(it->second.first, src, bytes, hipMemcpyHostToDevice));
+    if (std::string(name) == "beta_z0" || std::string(name) == "beta_z") h->beta_tables_internal = false;
+    return MPCMMD_OK;
+  });
+}
+
+int mpcmmd_run_stage(mpcmmd_handle* h, int32_t stage, int32_t t) {
+  if (!h) return fail(MPCMMD_E_INVALID, "null handle");
+  if (!h->begun) return fail(MPCMMD_E_STATE, "run_stage before mpcmmd_begin");
+  if (t < 0 || t >= h->T) return fail(MPCMMD_E_INVALID, "iteration out of range");
+  return guarded([&] {
+    check_device(h);
+    run_stage(h, stage, t);
+    if (stage == 3) h->last_t = t;
+    HIPC(hipStreamSynchronize(h->stream));
+    return MPCMMD_OK;
+  });
+}
+
+int mpcmmd_host_constant(const mpcmmd_config* cfg, const char* name, double* dst, size_t count) {
+  if (!cfg || !name) return fail(MPCMMD_E_INVALID, "null argument");
+  try {
+    ProblemConsts c = build_constants(cfg->num_prime, cfg->variant);
+    const std::vector<double>* v = nullptr;
+    std::string n(name);
+    if (n == "P") v = &c.P;
+    else if (n == "Pdot") v = &c.Pd;
+    else if (n == "Pddot") v = &c.Pdd;
+    else if (n == "P_prime") v = &c.P_prime;
+    else if (n == "P64") v = &c.P64;
+    else if (n == "Pdot64") v = &c.Pd64;
+    else if (n == "Pddot64") v = &c.Pdd64;
+    else if (n == "guess_kinv_x") v = &c.guess_kinv_x;
+    else if (n == "guess_kinv_y") v = &c.guess_kinv_y;
+    else if (n == "proj_kinv_x") v = &c.proj_kinv_x;
+    else if (n == "proj_kinv_y") v = &c.proj_kinv_y;
+    else if (n == "fit") v = &c.fit;
+    else return fail(MPCMMD_E_INVALID, "unknown constant " + n);
+    if (dst) {
+      if (count < v->size()) return fail(MPCMMD_E_INVALID, "dst too small");
+      std::memcpy(dst, v->data(), v->size() * 8);
+    }
+    return int(v->size());
+  } catch (const std::exception& e) {
+    return fail(MPCMMD_E_INVALID, e.what());
+  }
+}
+
+}  // extern "C"

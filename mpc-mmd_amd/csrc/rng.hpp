@@ -1,0 +1,111 @@
+// Counter-based RNG streams of the library (host + device).
+// Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11; Random123 round
+// constants), Box-Muller in fp64, Marsaglia-Tsang gamma in fp64, Beta as a
+// log-space gamma ratio.  The counter layout mirrors the reference's key
+// structure (fixed key for the initial population and the beta-CEM tables,
+// key 3*idx_mpc + 5*t + 7 per outer iteration: cem.py:225, cem_helper.py:86,
+// compute_beta.py:25) and is restated by oracle/rng.py for the parity tests.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.hpp"
+
+namespace mpcmmd {
+
+enum Stream : uint32_t {
+  kStreamRollAcc = 0,
+  kStreamRollSteer = 1,
+  kStreamRollConst = 2,
+  kStreamResample = 3,
+  kStreamGammaAccA = 4,
+  kStreamGammaAccB = 5,
+  kStreamGammaSteerA = 6,
+  kStreamGammaSteerB = 7,
+  kStreamPop0 = 16,
+  kStreamBetaZ0 = 17,
+  kStreamBetaZ = 18,
+};
+constexpr uint32_t kFixedKey0 = 0xFFFFFFFFu;
+constexpr int kGammaMaxAttempts = 32;
+
+struct U4 {
+  uint32_t x, y, z, w;
+};
+
+HDI U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = uint64_t(M0) * c.x;
+    const uint64_t p1 = uint64_t(M1) * c.z;
+    const uint32_t hi0 = uint32_t(p0 >> 32), lo0 = uint32_t(p0);
+    const uint32_t hi1 = uint32_t(p1 >> 32), lo1 = uint32_t(p1);
+    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+HDI uint32_t iteration_key0(int32_t idx_mpc, int32_t t) { return uint32_t(3 * idx_mpc + 5 * t + 7); }
+
+HDI double u01(uint32_t u) { return (double(u) + 0.5) * (1.0 / 4294967296.0); }
+
+// 4 normals of block j of stream (stream, word1): counter (j, word1, stream, 0)
+HDI void philox_normals4(uint32_t k0, uint32_t k1, uint32_t stream, uint32_t word1, uint32_t j, double out[4]) {
+  const U4 u = philox4x32_10(U4{j, word1, stream, 0u}, k0, k1);
+  const double two_pi = 6.283185307179586;
+  double r0 = sqrt(-2.0 * log(u01(u.x)));
+  double t0 = two_pi * u01(u.y);
+  double r1 = sqrt(-2.0 * log(u01(u.z)));
+  double t1 = two_pi * u01(u.w);
+  out[0] = r0 * cos(t0);
+  out[1] = r0 * sin(t0);
+  out[2] = r1 * cos(t1);
+  out[3] = r1 * sin(t1);
+}
+
+// Marsaglia-Tsang core (see oracle/rng.py:_log_gamma_parts): returns log G'
+// for alpha' = alpha (+1 when alpha < 1) and the boost log-uniform.
+DEVI void log_gamma_parts(double alpha, uint32_t k0, uint32_t k1, uint32_t stream, uint32_t elem,
+                          double& lg, double& lub) {
+  const double a1 = alpha < 1.0 ? alpha + 1.0 : alpha;
+  const double d = a1 - 1.0 / 3.0;
+  const double c = 1.0 / sqrt(9.0 * d);
+  const double two_pi = 6.283185307179586;
+  lg = log(d);
+  lub = 0.0;
+  for (int k = 0; k < kGammaMaxAttempts; ++k) {
+    const U4 u = philox4x32_10(U4{elem, uint32_t(k), stream, 1u}, k0, k1);
+    const double r = sqrt(-2.0 * log(u01(u.x)));
+    const double x = r * cos(two_pi * u01(u.y));
+    const double v = 1.0 + c * x;
+    if (v > 0.0) {
+      const double v3 = v * v * v;
+      const double lu = log(u01(u.z));
+      if (lu < 0.5 * x * x + d - d * v3 + d * log(v3)) {
+        lg = log(d * v3);
+        lub = log(u01(u.w));
+        return;
+      }
+    }
+  }
+}
+
+// Beta(a, b) with a = ra*s, b = rb*s (s = |control|); s == 0 takes the
+// alpha -> 0+ limit (oracle/rng.py:beta_draws, DESIGN.md Numerics).
+DEVI float beta_draw(double a, double b, double ra, double rb, uint32_t k0, uint32_t k1, uint32_t stream_a,
+                     uint32_t stream_b, uint32_t elem) {
+  double ga, ua, gb, ub;
+  log_gamma_parts(a, k0, k1, stream_a, elem, ga, ua);
+  log_gamma_parts(b, k0, k1, stream_b, elem, gb, ub);
+  if (a == 0.0 && b == 0.0) return (ua * rb > ub * ra) ? 1.0f : 0.0f;
+  const double la = a < 1.0 ? ga + ua / a : ga;
+  const double lb = b < 1.0 ? gb + ub / b : gb;
+  const double lm = la > lb ? la : lb;
+  const double ea = exp(la - lm), eb = exp(lb - lm);
+  return float(ea / (ea + eb));
+}
+
+}  // namespace mpcmmd

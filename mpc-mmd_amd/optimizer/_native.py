@@ -1,0 +1,236 @@
+"""ctypes binding of libmpcmmd.so (include/mpcmmd.h).
+
+The library is built in-tree (``mpc-mmd_amd/libmpcmmd.so``, see
+``__graft_entry__.build``).  There is no fallback: if the library is missing,
+or no GPU is visible when a handle is created, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MPCMMD_LIB", os.path.join(os.path.dirname(_HERE), "libmpcmmd.so"))
+
+COST = {"mmd_opt": 0, "mmd_random": 1, "cvar": 2, "saa": 3}
+NOISE = {"gaussian": 0, "beta": 1}
+VARIANT = {"static": 0, "dynamic": 1}
+RESULT_STRIDE_BETA_MAX = 32
+ABI_VERSION = 1
+
+SYMBOLS = (
+    "mpcmmd_abi_version", "mpcmmd_last_error", "mpcmmd_device_count", "mpcmmd_create",
+    "mpcmmd_destroy", "mpcmmd_set_stream", "mpcmmd_get_stream", "mpcmmd_solve", "mpcmmd_begin",
+    "mpcmmd_iterate", "mpcmmd_finish", "mpcmmd_sync", "mpcmmd_profile", "mpcmmd_kernel_times",
+    "mpcmmd_kernel_name", "mpcmmd_buffer_info", "mpcmmd_read", "mpcmmd_write", "mpcmmd_run_stage",
+    "mpcmmd_host_constant",
+)
+
+
+class Config(C.Structure):
+    _fields_ = [("num_reduced", C.c_int32), ("num_obs", C.c_int32), ("noise_level", C.c_float),
+                ("num_prime", C.c_int32), ("noise", C.c_int32), ("acc_const_noise", C.c_float),
+                ("steer_const_noise", C.c_float), ("num_batch", C.c_int32), ("variant", C.c_int32),
+                ("maxiter_cem", C.c_int32), ("device", C.c_int32), ("seed", C.c_uint32)]
+
+
+class Draws(C.Structure):
+    _fields_ = [("pop0", C.POINTER(C.c_float)), ("roll", C.POINTER(C.c_float)),
+                ("resample", C.POINTER(C.c_float)), ("beta_z0", C.POINTER(C.c_float)),
+                ("beta_z", C.POINTER(C.c_float))]
+
+
+class Result(C.Structure):
+    _fields_ = [("cx", C.c_float * 11), ("cy", C.c_float * 11), ("cost_lane", C.c_float),
+                ("cost_obs", C.c_float), ("sigma", C.c_float), ("res_beta", C.c_float * 20),
+                ("beta", C.POINTER(C.c_float)), ("elite_proj", C.POINTER(C.c_int32)),
+                ("elite_obs", C.POINTER(C.c_int32)), ("elite_cem", C.POINTER(C.c_int32))]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libmpcmmd.so once (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                          " (or `make -C mpc-mmd_amd`)")
+    L = C.CDLL(LIB_PATH)
+    fp = C.POINTER(C.c_float)
+    vp = C.c_void_p
+    L.mpcmmd_abi_version.restype = C.c_int32
+    L.mpcmmd_last_error.restype = C.c_char_p
+    L.mpcmmd_device_count.restype = C.c_int32
+    L.mpcmmd_create.argtypes = [C.POINTER(Config), C.POINTER(vp)]
+    L.mpcmmd_destroy.argtypes = [vp]
+    L.mpcmmd_destroy.restype = None
+    L.mpcmmd_set_stream.argtypes = [vp, vp]
+    L.mpcmmd_get_stream.argtypes = [vp]
+    L.mpcmmd_get_stream.restype = vp
+    args = [vp, C.c_int32, C.c_int32, fp, fp, fp, fp, fp, C.c_float, C.POINTER(Draws)]
+    L.mpcmmd_solve.argtypes = args + [C.POINTER(Result)]
+    L.mpcmmd_begin.argtypes = args
+    L.mpcmmd_iterate.argtypes = [vp, C.c_int32, C.c_int32]
+    L.mpcmmd_finish.argtypes = [vp, C.POINTER(Result)]
+    L.mpcmmd_sync.argtypes = [vp]
+    L.mpcmmd_profile.argtypes = [vp, C.c_int32]
+    L.mpcmmd_kernel_times.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_double), C.c_int32]
+    L.mpcmmd_kernel_name.argtypes = [C.c_int32]
+    L.mpcmmd_kernel_name.restype = C.c_char_p
+    L.mpcmmd_buffer_info.argtypes = [vp, C.c_char_p, C.POINTER(C.c_size_t)]
+    L.mpcmmd_read.argtypes = [vp, C.c_char_p, vp, C.c_size_t]
+    L.mpcmmd_write.argtypes = [vp, C.c_char_p, vp, C.c_size_t]
+    L.mpcmmd_run_stage.argtypes = [vp, C.c_int32, C.c_int32]
+    L.mpcmmd_host_constant.argtypes = [C.POINTER(Config), C.c_char_p, C.POINTER(C.c_double), C.c_size_t]
+    if L.mpcmmd_abi_version() != ABI_VERSION:
+        raise NativeError("libmpcmmd ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc < 0:
+        raise NativeError(f"libmpcmmd error {rc}: {lib().mpcmmd_last_error().decode()}")
+    return rc
+
+
+def make_config(num_reduced, num_obs, noise_level, num_prime, noise, acc_const_noise, steer_const_noise,
+                num_batch=100, variant="static", maxiter_cem=20, device=0, seed=0):
+    return Config(int(num_reduced), int(num_obs), float(noise_level), int(num_prime), NOISE[noise],
+                  float(acc_const_noise), float(steer_const_noise), int(num_batch), VARIANT[variant],
+                  int(maxiter_cem), int(device), int(seed) & 0xFFFFFFFF)
+
+
+def host_constant(cfg, name):
+    L = lib()
+    n = check(L.mpcmmd_host_constant(C.byref(cfg), name.encode(), None, 0))
+    out = np.empty(n, np.float64)
+    check(L.mpcmmd_host_constant(C.byref(cfg), name.encode(), out.ctypes.data_as(C.POINTER(C.c_double)), n))
+    return out
+
+
+def _fptr(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+class Handle:
+    """Owns one mpcmmd_handle (one device, one stream)."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self._L = lib()
+        if self._L.mpcmmd_device_count() < 1:
+            raise NativeError("no HIP device visible: libmpcmmd needs an MI355X (gfx950)")
+        h = C.c_void_p()
+        check(self._L.mpcmmd_create(C.byref(cfg), C.byref(h)))
+        self._h = h
+        self._keep = []
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.mpcmmd_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- solve ----------------------------------------------------------------
+    def _inputs(self, init_state, mean, cov, x_obs, y_obs, draws):
+        f = lambda a: np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+        ins = dict(init_state=f(init_state).reshape(6), mean=f(mean).reshape(8), cov=f(cov).reshape(64),
+                   x_obs=f(x_obs), y_obs=f(y_obs))
+        if ins["x_obs"].shape != (self.cfg.num_obs, 100) or ins["y_obs"].shape != (self.cfg.num_obs, 100):
+            raise ValueError(f"x_obs_traj / y_obs_traj must be [{self.cfg.num_obs}, 100]")
+        d = None
+        if draws is not None:
+            keep = {}
+            for k in ("pop0", "roll", "resample", "beta_z0", "beta_z"):
+                a = getattr(draws, k, None)
+                keep[k] = None if a is None else np.ascontiguousarray(a, dtype=np.float32)
+            d = Draws(*(_fptr(keep[k]) for k in ("pop0", "roll", "resample", "beta_z0", "beta_z")))
+            ins["_draws_keep"] = keep
+        ins["draws"] = d
+        return ins
+
+    def begin(self, cost, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des, draws=None):
+        ins = self._inputs(init_state, mean, cov, x_obs, y_obs, draws)
+        self._keep = [ins]
+        d = ins["draws"]
+        check(self._L.mpcmmd_begin(self._h, COST[cost], int(idx_mpc), _fptr(ins["init_state"]),
+                                   _fptr(ins["mean"]), _fptr(ins["cov"]), _fptr(ins["x_obs"]),
+                                   _fptr(ins["y_obs"]), float(v_des), None if d is None else C.byref(d)))
+
+    def iterate(self, t_begin, count):
+        check(self._L.mpcmmd_iterate(self._h, int(t_begin), int(count)))
+
+    def sync(self):
+        check(self._L.mpcmmd_sync(self._h))
+
+    def finish(self, trace=False):
+        r = Result()
+        beta = np.zeros(max(self.cfg.num_reduced, 1), np.float32)
+        r.beta = _fptr(beta)
+        T, B = self.cfg.maxiter_cem, self.cfg.num_batch
+        tr = None
+        if trace:
+            tr = dict(elite_proj=np.zeros((T, B), np.int32), elite_obs=np.zeros((T, 20), np.int32),
+                      elite_cem=np.zeros((T, 5), np.int32))
+            for k, v in tr.items():
+                setattr(r, k, v.ctypes.data_as(C.POINTER(C.c_int32)))
+        check(self._L.mpcmmd_finish(self._h, C.byref(r)))
+        out = dict(cx=np.array(r.cx, np.float32), cy=np.array(r.cy, np.float32),
+                   cost_lane=np.float32(r.cost_lane), cost_obs=np.float32(r.cost_obs),
+                   sigma=np.float32(r.sigma), res_beta=np.array(r.res_beta, np.float32), beta=beta)
+        if tr is not None:
+            out.update(tr)
+        return out
+
+    def solve(self, cost, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des, draws=None, trace=False):
+        self.begin(cost, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des, draws)
+        self.iterate(0, self.cfg.maxiter_cem)
+        return self.finish(trace)
+
+    # -- stage access (parity tests) -------------------------------------------
+    def buffer_bytes(self, name):
+        n = C.c_size_t()
+        check(self._L.mpcmmd_buffer_info(self._h, name.encode(), C.byref(n)))
+        return n.value
+
+    def read(self, name, dtype=np.float32, shape=None):
+        nb = self.buffer_bytes(name)
+        out = np.empty(nb // np.dtype(dtype).itemsize, dtype)
+        check(self._L.mpcmmd_read(self._h, name.encode(), out.ctypes.data, out.nbytes))
+        return out if shape is None else out[: int(np.prod(shape))].reshape(shape)
+
+    def write(self, name, arr):
+        arr = np.ascontiguousarray(arr)
+        check(self._L.mpcmmd_write(self._h, name.encode(), arr.ctypes.data, arr.nbytes))
+
+    def run_stage(self, stage, t):
+        check(self._L.mpcmmd_run_stage(self._h, int(stage), int(t)))
+
+    # -- streams / profiling -----------------------------------------------------
+    def set_stream(self, stream_ptr):
+        check(self._L.mpcmmd_set_stream(self._h, C.c_void_p(stream_ptr)))
+
+    def profile(self, enable):
+        check(self._L.mpcmmd_profile(self._h, 1 if enable else 0))
+
+    def kernel_times(self):
+        n = 16
+        la = (C.c_int32 * n)()
+        ms = (C.c_double * n)()
+        k = check(self._L.mpcmmd_kernel_times(self._h, la, ms, n))
+        return {self._L.mpcmmd_kernel_name(i).decode(): (la[i], ms[i]) for i in range(k)}

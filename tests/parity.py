@@ -1,0 +1,80 @@
+"""Shared helpers for GPU-vs-oracle parity tests.
+
+Tolerance contract (Numerics): costs and trajectories within
+1e-4 relative (with an absolute floor for values near 0); elite index sets
+bit-exact unless the compared keys are a near-tie (within tolerance), in
+which case the difference is reported, not hidden.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import oracle
+from oracle.helper import compute_obs_trajectories
+
+RTOL = 1e-4
+
+
+def close(name, got, ref, rtol=RTOL, atol=1e-5, frac_ok=0.0):
+    """Assert |got - ref| <= atol + rtol |ref| elementwise (NaN == NaN).
+    ``frac_ok``: tolerated fraction of mismatching elements (rejection-
+    sampled Beta draws, documented)."""
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    assert got.shape == ref.shape, f"{name}: shape {got.shape} vs {ref.shape}"
+    both_nan = np.isnan(got) & np.isnan(ref)
+    err = np.abs(got - ref)
+    bad = ~both_nan & ~(err <= atol + rtol * np.abs(ref))
+    if bad.mean() > frac_ok:
+        i = np.argwhere(bad)[:5]
+        detail = [(tuple(j), got[tuple(j)], ref[tuple(j)]) for j in i]
+        raise AssertionError(f"{name}: {bad.sum()}/{bad.size} outside tol; worst {np.nanmax(err):.3g}; {detail}")
+    return float(np.nanmax(np.where(both_nan, 0, err))) if err.size else 0.0
+
+
+def elite_equal(name, got, ref, keys, tol=RTOL):
+    """Index sets must agree; where they differ, every differing candidate's
+    key must be within ``tol`` (relative) of the boundary key."""
+    got = np.asarray(got)
+    ref = np.asarray(ref)
+    if np.array_equal(got, ref):
+        return True
+    keys = np.asarray(keys, np.float64)
+    bound = keys[ref[-1]]
+    diff = np.setxor1d(got, ref)
+    scale = max(abs(bound), 1e-6)
+    near = np.all(np.abs(keys[diff] - bound) <= tol * scale + 1e-6)
+    if np.array_equal(np.sort(got), np.sort(ref)):
+        # same set, different order: order ties must be near-ties too
+        pos = np.nonzero(got != ref)[0]
+        near = np.all(np.abs(keys[got[pos]] - keys[ref[pos]]) <= tol * np.maximum(np.abs(keys[ref[pos]]), 1e-6) + 1e-6)
+    assert near, f"{name}: index sets differ beyond a near-tie: got {got} ref {ref}"
+    return False
+
+
+def scenario(num_obs, seed=0):
+    """Static-obstacle scenario like S/main_mpc.py:10-21 on an extended x grid
+    (the reference's 9-slot grid cannot place > 9 obstacles)."""
+    rng = np.random.RandomState(seed)
+    xs = np.arange(35, 35 + 5 * max(9, num_obs), 5, dtype=np.float64)
+    x = rng.choice(xs, num_obs, replace=False)
+    y = rng.choice(np.array([-1.75, 1.75]), num_obs)
+    z = np.zeros(num_obs)
+    return x, y, z, z, z
+
+
+DEFAULT_INIT = np.array([0.0, 1.75, 5.0, 0.0, 0.0, 0.0], np.float32)   # S/main_mpc.py:46-54
+DEFAULT_MEAN = np.array([15] * 4 + [0] * 4, np.float32)                 # S/main_mpc.py:58-71
+DEFAULT_COV = np.diag([20.0] * 4 + [100.0] * 4).astype(np.float32)      # S/main_mpc.py:69-74
+
+
+def make_pair(native, cost, noise="gaussian", n=16, O=3, H=10, B=32, T=3, level=None, variant="static",
+              acc_c=0.0, steer_c=0.0, seed=0):
+    level = (0.1 if noise == "gaussian" else 0.3) if level is None else level
+    ora = oracle.CEM(n, O, level, H, noise, acc_c, steer_c, num_batch=B, variant=variant, maxiter_cem=T)
+    cfg = native.make_config(n, O, level, H, noise, acc_c, steer_c, num_batch=B, variant=variant,
+                             maxiter_cem=T, device=0, seed=seed)
+    nat = native.Handle(cfg)
+    x, y, vx, vy, psi = scenario(O, seed)
+    xo, yo, _ = compute_obs_trajectories(ora.prob, x, y, vx, vy, psi)
+    return ora, nat, xo, yo
