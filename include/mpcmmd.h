@@ -165,7 +165,16 @@ int mpcmmd_write(mpcmmd_handle* h, const char* name, const void* src, size_t byt
  *   2 risk       noisy rollouts + collision residual + risk reducer per candidate
  *                (cem_helper.py:402-538, costs.py:50-234, compute_beta.py:93-157)
  *   3 select     argsorts, compute_cost, elites, compute_shifted_samples
- *                (cem.py:233-315, cem_helper.py:232-314) */
+ *                (cem.py:233-315, cem_helper.py:232-314)
+ * cost = mmd_opt splits stage 2 into sub-stages (t = outer iteration for 4, 8;
+ * t = beta-CEM iteration 0..19 for 5-7):
+ *   4 mother     noisy rows, n^2 mother rollouts, Bernstein fit (cem_helper.py:469-564)
+ *   5 bsample    beta-CEM samples + top-n |beta| rows     (compute_beta.py:41-68, 117-118)
+ *   6 bkernel    kernel row sums, reduced QP, QP cost     (compute_beta.py:70-91, 120-129)
+ *   7 belite     elites, mean, next generators             (compute_beta.py:51-68, 133-157)
+ *   8 mmdfinal   reduced rollouts, MMD obs / lane          (costs.py:121-135, 173-186)
+ * Buffer "beta_z" holds the device layout [20][M+1][89] (transposed on
+ * upload in mpcmmd_begin; mpcmmd_write writes it raw). */
 int mpcmmd_run_stage(mpcmmd_handle* h, int32_t stage, int32_t t);
 
 /* Host-side batch-invariant constants (no GPU needed): fills dst with the

@@ -17,12 +17,11 @@
 #include "block.hpp"
 #include "kernels.hpp"
 #include "rng.hpp"
+#include "rollout.hpp"
 
 namespace mpcmmd {
 
 namespace {
-
-constexpr float kA2 = 18.0625f, kB2 = 7.5625f;  // 4.25^2, 2.75^2 (exact in fp32)
 
 struct RiskLds {
   float* xo;
@@ -69,30 +68,6 @@ size_t risk_lds_bytes(int O, int H, int S) {
   return f + sizeof(ReduceScratch);
 }
 
-// Noisy controls of sample row r at step h (cem_helper.py:414-443 / 478-508).
-DEVI void noisy_control(const Params& p, int t, int r, int h, float a, float s, float& an, float& sn) {
-  const int S = p.S, H = p.H;
-  const float* roll = p.roll + size_t(t) * 3 * H * S;
-  const float nc = roll[(2 * H + h) * S + r];
-  float ap, sp;
-  if (p.noise == 0) {
-    ap = (p.sigma_acc * fabsf(a)) * roll[(0 * H + h) * S + r];
-    sp = (p.sigma_steer * fabsf(s)) * roll[(1 * H + h) * S + r];
-  } else {
-    const uint32_t k0 = iteration_key0(p.idx_mpc, t), k1 = p.seed;
-    const uint32_t elem = uint32_t(r) * uint32_t(H) + uint32_t(h);
-    const float fa = fabsf(a), fs = fabsf(s);
-    const float nba = beta_draw(double(2.0f * fa), double(5.0f * fa), 2.0, 5.0, k0, k1, kStreamGammaAccA,
-                                kStreamGammaAccB, elem);
-    const float nbs = beta_draw(double(2.0f * fs), double(5.0f * fs), 2.0, 5.0, k0, k1, kStreamGammaSteerA,
-                                kStreamGammaSteerB, elem);
-    ap = p.sigma_acc * (2.0f * nba - 1.0f);
-    sp = p.K_steer * (2.0f * nbs - 1.0f);  // K_steer holds float32(K_steer * sigma_steer)
-  }
-  an = (a + ap) + p.acc_const * nc;
-  sn = (s + sp) + p.steer_const * nc;
-}
-
 namespace {
 
 __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
@@ -109,8 +84,6 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
     L.st[h] = p.steer[size_t(b) * 100 + h];
   }
   __syncthreads();
-  const float dt = 0.15f, wb = 2.5f, rwb = 1.0f / 2.5f;
-  const float ra2 = 1.0f / kA2, rb2 = 1.0f / kB2;
   for (int r = threadIdx.x; r < S; r += blockDim.x) {
     float x = p.st0[0], y = p.st0[1], vx = p.st0[2], vy = p.st0[3], psi = p.st0[4];
     float cb = 0.0f, lb = 0.0f, ub = 0.0f;
@@ -118,9 +91,7 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
     for (int h = 0; h < H; ++h) {
       // residual of the recorded state (x_roll[:, h] = state before step h)
       for (int o = 0; o < O; ++o) {
-        const float wc = x - L.xo[o * H + h];
-        const float ws = y - L.yo[o * H + h];
-        const float c = (-div_rc(wc * wc, kA2, ra2) - div_rc(ws * ws, kB2, rb2)) + 1.0f;
+        const float c = f_bar(x, y, L.xo[o * H + h], L.yo[o * H + h]);
         nan |= (c != c);
         cb = fmaxf(cb, c);
       }
@@ -131,14 +102,7 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
       if (h == H - 1) break;  // the last step's state is never recorded
       float an, sn;
       noisy_control(p, t, r, h, L.a[h], L.st[h], an, sn);
-      float v = sqrtf(vx * vx + vy * vy);
-      v = v + an * dt;
-      const float psidot = div_rc(v * tanf(sn), wb, rwb);
-      psi = psi + psidot * dt;
-      vx = v * cosf(psi);
-      vy = v * sinf(psi);
-      x = x + vx * dt;
-      y = y + vy * dt;
+      bicycle_step(x, y, vx, vy, psi, an, sn);
     }
     const float qnan = __int_as_float(0x7fc00000);
     L.cbar[r] = nan ? qnan : cb;

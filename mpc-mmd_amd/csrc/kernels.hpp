@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace mpcmmd {
 
 constexpr int kMaxH = 100;
@@ -14,6 +16,7 @@ constexpr int kBetaElite = 11;         // compute_beta.py:26
 constexpr int kEliteCost = 20;         // cem.py:140
 constexpr int kElite = 5;              // cem.py:138
 constexpr int kResultStride = 11 + 11 + 2 + 1 + 20 + kMaxReduced;  // cx, cy, lane, obs, sigma, res_beta, beta
+constexpr int kGenStride = 24;         // doubles per position in Params::gen
 
 struct Params {
   // shapes / configuration
@@ -57,6 +60,17 @@ struct Params {
   float* beta;             // [B][n]
   float* sigma;            // [B]
   float* res_beta;         // [B][20]
+  // mmd_opt scratch (beta-CEM, compute_beta.py:93-157)
+  float* feat;             // [B][22][M]   mother Bernstein coefficients (cx | cy)
+  float* ctrl_n;           // [B][2][n][H] noisy control rows (acc, steer)
+  int32_t* bsel;           // [B][100][n]  top-n |beta| indices (argsort order)
+  float* bsig;             // [B][100]     sample sigma (last coordinate, clipped)
+  float* btop;             // [B][100][n]  QP solutions
+  float* bcost;            // [B][100]     QP costs
+  float* belite;           // [2][B][11][M+1] elite sample vectors (ping-pong)
+  double* gen;             // [B][M+1][kGenStride] W (11), U (11), L_jj
+  float* genm;             // [B][M+1]     float32 elite mean
+  int32_t* bestsel;        // [B][n]       reduced set of the best sample
   // outputs
   float* results;          // [T][kResultStride]
   int32_t* tr_proj;        // [T][B]
@@ -66,9 +80,13 @@ struct Params {
 
 void launch_noise(const Params& p, int t, hipStream_t s);
 void launch_front(const Params& p, int t, hipStream_t s);
-void launch_risk(const Params& p, int t, hipStream_t s);
 void launch_select(const Params& p, int t, hipStream_t s);
-void launch_init_pop(const Params& p, hipStream_t s);
-void launch_fill_fixed(const Params& p, hipStream_t s);
-
+void launch_risk_baseline(const Params& p, int t, hipStream_t s);
+// mmd_opt risk, one launch each (mpcmmd.hip chains them)
+void launch_mother(const Params& p, int t, hipStream_t s);
+void launch_bsample(const Params& p, int tb, hipStream_t s);
+void launch_bkernel(const Params& p, int tb, hipStream_t s);
+void launch_belite(const Params& p, int tb, hipStream_t s);
+void launch_mmdfinal(const Params& p, int t, hipStream_t s);
+bool mmdopt_supported(int n, int H, int O, std::string* why);
 }  // namespace mpcmmd

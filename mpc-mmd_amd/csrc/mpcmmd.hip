@@ -17,12 +17,6 @@
 #include "kernels.hpp"
 #include "rng.hpp"
 
-namespace mpcmmd {
-void launch_risk_baseline(const Params& p, int t, hipStream_t s);
-void launch_risk_mmdopt(const Params& p, int t, hipStream_t s);
-size_t mmdopt_lds_bytes(const Params& p);
-}  // namespace mpcmmd
-
 using namespace mpcmmd;
 
 namespace {
@@ -46,8 +40,20 @@ struct HipError : std::runtime_error {
                      std::to_string(__LINE__) + ")");                                              \
   } while (0)
 
-enum KernelId { kKNoise = 0, kKFront, kKRiskBaseline, kKRiskMmdOpt, kKSelect, kNumKernels };
-const char* kKernelNames[kNumKernels] = {"noise", "front", "risk_baseline", "risk_mmdopt", "select"};
+enum KernelId {
+  kKNoise = 0,
+  kKFront,
+  kKRiskBaseline,
+  kKMother,
+  kKBSample,
+  kKBKernel,
+  kKBElite,
+  kKMmdFinal,
+  kKSelect,
+  kNumKernels
+};
+const char* kKernelNames[kNumKernels] = {"noise",   "front",  "risk_baseline", "mother", "bsample",
+                                         "bkernel", "belite", "mmdfinal",      "select"};
 
 }  // namespace
 
@@ -66,6 +72,8 @@ struct mpcmmd_handle {
   int last_t = -1;
   bool ext_roll = false, ext_res = false;
   bool beta_tables_internal = false;  // device beta tables hold the internal streams
+  bool mmd_ok = false;                // mmd_opt buffers allocated (mmdopt_supported)
+  std::string mmd_why;
   // profiling
   bool prof = false;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -157,15 +165,25 @@ void upload(mpcmmd_handle* h, const char* name, const void* src, size_t bytes, s
   HIPC(hipMemcpyAsync(static_cast<char*>(it->second.first) + offset, src, bytes, hipMemcpyHostToDevice, h->stream));
 }
 
+// beta_z iteration t: [89][M+1] (draw order) -> device [M+1][89], so the
+// generation kernels read one position for 64 samples in one transaction
+void upload_beta_z(mpcmmd_handle* h, int t, const float* z) {
+  const int M1 = h->M + 1, R = kBetaSamples - kBetaElite;
+  std::vector<float> tr(size_t(R) * M1);
+  for (int r = 0; r < R; ++r)
+    for (int j = 0; j < M1; ++j) tr[size_t(j) * R + r] = z[size_t(r) * M1 + j];
+  upload(h, "beta_z", tr.data(), tr.size() * 4, size_t(t) * tr.size() * 4);
+  HIPC(hipStreamSynchronize(h->stream));  // tr is a host temporary
+}
+
 void gen_beta_tables(mpcmmd_handle* h) {
   const int M1 = h->M + 1;
   const uint32_t k0 = kFixedKey0, k1 = h->cfg.seed;
   auto z0 = host_normals(k0, k1, kStreamBetaZ0, 0, size_t(kBetaSamples) * M1);
   upload(h, "beta_z0", z0.data(), z0.size() * 4);
-  const size_t per = size_t(kBetaSamples - kBetaElite) * M1;
   for (int t = 0; t < kBetaIters; ++t) {
-    auto z = host_normals(k0, k1, kStreamBetaZ, uint32_t(t), per);
-    upload(h, "beta_z", z.data(), per * 4, size_t(t) * per * 4);
+    auto z = host_normals(k0, k1, kStreamBetaZ, uint32_t(t), size_t(kBetaSamples - kBetaElite) * M1);
+    upload_beta_z(h, t, z.data());
   }
   HIPC(hipStreamSynchronize(h->stream));
   h->beta_tables_internal = true;
@@ -181,16 +199,36 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
       h->launch(kKFront, [&] { launch_front(p, t, h->stream); });
       break;
     case 2:
-      if (p.cost == MPCMMD_COST_MMD_OPT)
-        h->launch(kKRiskMmdOpt, [&] { launch_risk_mmdopt(p, t, h->stream); });
-      else
+      if (p.cost == MPCMMD_COST_MMD_OPT) {
+        if (!h->mmd_ok) throw std::invalid_argument("mmd_opt unsupported for this configuration: " + h->mmd_why);
+        h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
+        for (int tb = 0; tb < kBetaIters; ++tb) {
+          h->launch(kKBSample, [&] { launch_bsample(p, tb, h->stream); });
+          h->launch(kKBKernel, [&] { launch_bkernel(p, tb, h->stream); });
+          h->launch(kKBElite, [&] { launch_belite(p, tb, h->stream); });
+        }
+        h->launch(kKMmdFinal, [&] { launch_mmdfinal(p, t, h->stream); });
+      } else
         h->launch(kKRiskBaseline, [&] { launch_risk_baseline(p, t, h->stream); });
       break;
     case 3:
       h->launch(kKSelect, [&] { launch_select(p, t, h->stream); });
       break;
+    case 4:
+    case 5:
+    case 6:
+    case 7:
+    case 8:
+      if (p.cost != MPCMMD_COST_MMD_OPT || !h->mmd_ok) throw std::invalid_argument("stages 4-8 need cost mmd_opt");
+      if (stage >= 5 && stage <= 7 && t >= kBetaIters) throw std::invalid_argument("beta-CEM iteration out of range");
+      if (stage == 4) h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
+      if (stage == 5) h->launch(kKBSample, [&] { launch_bsample(p, t, h->stream); });
+      if (stage == 6) h->launch(kKBKernel, [&] { launch_bkernel(p, t, h->stream); });
+      if (stage == 7) h->launch(kKBElite, [&] { launch_belite(p, t, h->stream); });
+      if (stage == 8) h->launch(kKMmdFinal, [&] { launch_mmdfinal(p, t, h->stream); });
+      break;
     default:
-      throw std::invalid_argument("stage must be 0..3");
+      throw std::invalid_argument("stage must be 0..8");
   }
 }
 
@@ -250,7 +288,8 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
     h->M = c.num_reduced * c.num_reduced;
     h->T = c.maxiter_cem;
     const int B = h->B, S = h->S, H = h->H, O = h->O, T = h->T;
-    const bool mmd_ok = h->n <= kMaxReduced;
+    const bool mmd_ok = mmdopt_supported(h->n, h->H, h->O, &h->mmd_why);
+    h->mmd_ok = mmd_ok;
     Params& p = h->p;
     p.B = B;
     p.S = S;
@@ -309,6 +348,17 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
     if (mmd_ok) {
       p.beta_z0 = (const float*)h->alloc("beta_z0", size_t(kBetaSamples) * (h->M + 1) * 4);
       p.beta_z = (const float*)h->alloc("beta_z", size_t(kBetaIters) * (kBetaSamples - kBetaElite) * (h->M + 1) * 4);
+      const size_t M = h->M, M1 = M + 1, n = h->n;
+      p.feat = (float*)h->alloc("feat", size_t(B) * 22 * M * 4);
+      p.ctrl_n = (float*)h->alloc("ctrl_n", size_t(B) * 2 * n * H * 4);
+      p.bsel = (int32_t*)h->alloc("bsel", size_t(B) * kBetaSamples * n * 4);
+      p.bsig = (float*)h->alloc("bsig", size_t(B) * kBetaSamples * 4);
+      p.btop = (float*)h->alloc("btop", size_t(B) * kBetaSamples * n * 4);
+      p.bcost = (float*)h->alloc("bcost", size_t(B) * kBetaSamples * 4);
+      p.belite = (float*)h->alloc("belite", size_t(2) * B * kBetaElite * M1 * 4);
+      p.gen = (double*)h->alloc("gen", size_t(B) * M1 * kGenStride * 8);
+      p.genm = (float*)h->alloc("genm", size_t(B) * M1 * 4);
+      p.bestsel = (int32_t*)h->alloc("bestsel", size_t(B) * n * 4);
     }
     p.pop = (float*)h->alloc("pop", size_t(2) * B * 8 * 4);
     p.mean = (float*)h->alloc("mean", 8 * 4);
@@ -379,8 +429,7 @@ int mpcmmd_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const flo
                  const mpcmmd_draws* draws) {
   if (!h || !init_state || !mean || !cov || !x_obs || !y_obs) return fail(MPCMMD_E_INVALID, "null argument");
   if (cost_kind < 0 || cost_kind > 3) return fail(MPCMMD_E_INVALID, "cost_kind must be 0..3");
-  if (cost_kind == MPCMMD_COST_MMD_OPT && h->n > kMaxReduced)
-    return fail(MPCMMD_E_UNSUPPORTED, "mmd_opt needs num_reduced <= 32 (M = n^2 <= 1024)");
+  if (cost_kind == MPCMMD_COST_MMD_OPT && !h->mmd_ok) return fail(MPCMMD_E_UNSUPPORTED, h->mmd_why);
   return guarded([&] {
     check_device(h);
     Params& p = h->p;
@@ -455,7 +504,8 @@ int mpcmmd_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const flo
       if (ext_b) {
         if (!draws->beta_z0 || !draws->beta_z) throw std::invalid_argument("beta_z0 and beta_z go together");
         upload(h, "beta_z0", draws->beta_z0, size_t(kBetaSamples) * M1 * 4);
-        upload(h, "beta_z", draws->beta_z, size_t(kBetaIters) * (kBetaSamples - kBetaElite) * M1 * 4);
+        for (int t = 0; t < kBetaIters; ++t)
+          upload_beta_z(h, t, draws->beta_z + size_t(t) * (kBetaSamples - kBetaElite) * M1);
         h->beta_tables_internal = false;
       } else if (!h->beta_tables_internal) {
         gen_beta_tables(h);
@@ -605,7 +655,8 @@ int mpcmmd_write(mpcmmd_handle* h, const char* name, const void* src, size_t byt
 int mpcmmd_run_stage(mpcmmd_handle* h, int32_t stage, int32_t t) {
   if (!h) return fail(MPCMMD_E_INVALID, "null handle");
   if (!h->begun) return fail(MPCMMD_E_STATE, "run_stage before mpcmmd_begin");
-  if (t < 0 || t >= h->T) return fail(MPCMMD_E_INVALID, "iteration out of range");
+  const bool beta_stage = stage >= 5 && stage <= 7;
+  if (t < 0 || (!beta_stage && t >= h->T)) return fail(MPCMMD_E_INVALID, "iteration out of range");
   return guarded([&] {
     check_device(h);
     run_stage(h, stage, t);

@@ -1,0 +1,59 @@
+// Device pieces shared by the rollout kernels (baseline risk and mmd_opt).
+#pragma once
+#include "common.hpp"
+#include "kernels.hpp"
+#include "rng.hpp"
+
+namespace mpcmmd {
+
+constexpr float kDt = 0.15f;         // cem.py:40
+constexpr float kWheelBase = 2.5f;   // cem.py:26
+
+// Noisy controls of noise row r at step h of outer iteration t
+// (cem_helper.py:405-443 baseline / 469-508 opt; one realisation shared by
+// every candidate, Q2).  Gaussian rows come from p.roll [T][3][H][S]; Beta
+// draws from the Philox gamma streams (elements r*H + h).
+DEVI void noisy_control(const Params& p, int t, int r, int h, float a, float s, float& an, float& sn) {
+  const int S = p.S, H = p.H;
+  const float* roll = p.roll + size_t(t) * 3 * H * S;
+  const float nc = roll[(2 * H + h) * S + r];
+  float ap, sp;
+  if (p.noise == 0) {
+    ap = (p.sigma_acc * fabsf(a)) * roll[(0 * H + h) * S + r];
+    sp = (p.sigma_steer * fabsf(s)) * roll[(1 * H + h) * S + r];
+  } else {
+    const uint32_t k0 = iteration_key0(p.idx_mpc, t), k1 = p.seed;
+    const uint32_t elem = uint32_t(r) * uint32_t(H) + uint32_t(h);
+    const float fa = fabsf(a), fs = fabsf(s);
+    const float nba = beta_draw(double(2.0f * fa), double(5.0f * fa), 2.0, 5.0, k0, k1, kStreamGammaAccA,
+                                kStreamGammaAccB, elem);
+    const float nbs = beta_draw(double(2.0f * fs), double(5.0f * fs), 2.0, 5.0, k0, k1, kStreamGammaSteerA,
+                                kStreamGammaSteerB, elem);
+    ap = p.sigma_acc * (2.0f * nba - 1.0f);
+    sp = p.K_steer * (2.0f * nbs - 1.0f);  // K_steer holds float32(K_steer * sigma_steer)
+  }
+  an = (a + ap) + p.acc_const * nc;
+  sn = (s + sp) + p.steer_const * nc;
+}
+
+// compute_rollout_one_step (cem_helper.py:380-400), fp32 in reference order.
+// psidot = v tan(steer) / 2.5: division by 2.5 via the exact fma form.
+DEVI void bicycle_step(float& x, float& y, float& vx, float& vy, float& psi, float an, float sn) {
+  float v = sqrtf(vx * vx + vy * vy);
+  v = v + an * kDt;
+  const float psidot = div_rc(v * tanf(sn), kWheelBase, 1.0f / kWheelBase);
+  psi = psi + psidot * kDt;
+  vx = v * cosf(psi);
+  vy = v * sinf(psi);
+  x = x + vx * kDt;
+  y = y + vy * kDt;
+}
+
+// compute_f_bar (costs.py:50-60): ((-(dx^2))/a^2 - dy^2/b^2) + 1
+DEVI float f_bar(float x, float y, float xo, float yo) {
+  constexpr float kA2 = 18.0625f, kB2 = 7.5625f;  // 4.25^2, 2.75^2 (exact in fp32)
+  const float wc = x - xo, ws = y - yo;
+  return (-div_rc(wc * wc, kA2, 1.0f / kA2) - div_rc(ws * ws, kB2, 1.0f / kB2)) + 1.0f;
+}
+
+}  // namespace mpcmmd

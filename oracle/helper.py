@@ -193,13 +193,19 @@ def mother_controls(acc_n, steer_n):
 
 def compute_coeff(prob, x, y):
     """``Helper.compute_coeff`` (cem_helper.py:553-564): ridge fit to the
-    horizon basis, c = (P'^T P' + 0.05 I)^-1 P'^T x (fp64 solve)."""
-    Pp = prob.P_prime.astype(F64)
-    rx = Pp.T @ np.asarray(x, F64).reshape(-1, x.shape[-1]).T
-    ry = Pp.T @ np.asarray(y, F64).reshape(-1, y.shape[-1]).T
-    cx = np.linalg.solve(prob.fit_cost, rx).T
-    cy = np.linalg.solve(prob.fit_cost, ry).T
-    return f32(cx).reshape(x.shape[:-1] + (11,)), f32(cy).reshape(y.shape[:-1] + (11,))
+    horizon basis, c = (P'^T P' + 0.05 I)^-1 P'^T x.  The batch-invariant
+    matrix Fit = (P'^T P' + 0.05 I)^-1 P'^T [11, H] is built once
+    (problem.py) and applied in fp64, sequentially over the horizon (the GPU
+    folds it into the rollout scan in the same order)."""
+    fit = prob.fit
+    cx = np.zeros(x.shape[:-1] + (11,))
+    cy = np.zeros(y.shape[:-1] + (11,))
+    xd = np.asarray(x, F64)
+    yd = np.asarray(y, F64)
+    for h in range(x.shape[-1]):
+        cx = cx + fit[:, h] * xd[..., h:h + 1]
+        cy = cy + fit[:, h] * yd[..., h:h + 1]
+    return f32(cx), f32(cy)
 
 
 def _norm(x):

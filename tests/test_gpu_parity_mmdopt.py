@@ -1,0 +1,167 @@
+"""GPU parity of the mmd_opt path (nested beta-CEM) against the oracle.
+
+Sub-stage lockstep (run_stage 4-8): the oracle is fed the GPU's inputs of
+each sub-stage and must reproduce its outputs:
+  mother    noisy rows + mother rollouts + Bernstein fit  -> ctrl_n, feat
+  bsample   samples (elites of the previous iteration + mean + L z with the
+            dense fp64 Cholesky of jnp.cov + 0.05 I) -> top-n |beta| rows, sigma
+  bkernel   Laplace kernels, reduced QP, QP cost          -> btop, bcost
+  belite    elite 11 by cost                              -> elite sample rows
+  mmdfinal  reduced rollouts + MMD obs / lane             -> obs_cost, lane_cost
+Selections (integer index sets) must agree exactly unless the compared keys
+are a near-tie; floating outputs within tolerances stated per check.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from oracle import beta_cem as bc
+from oracle import costs as C
+from oracle import helper as Hh
+from parity import DEFAULT_COV, DEFAULT_INIT, DEFAULT_MEAN, close, elite_equal, make_pair
+
+pytestmark = pytest.mark.gpu
+
+F32, F64 = np.float32, np.float64
+SQRT20 = np.sqrt(20.0)
+
+
+def _samples_from_elites(E, z_t, M, clip=0.01):
+    """Rows 11..99 of the next samples from the 11 elite rows E [11, M+1]
+    (compute_beta.py:51-68): mean, jnp.cov + 0.05 I, dense Cholesky."""
+    El = E.astype(F64)
+    mean64 = El.mean(axis=0)
+    mean32 = mean64.astype(F32)
+    D = El - mean64
+    cov = D.T @ D / 10.0 + 0.05 * np.eye(M + 1)
+    L = Hh.chol64(cov)
+    new = (mean32.astype(F64) + z_t.astype(F64) @ L.T).astype(F32)
+    new[:, M] = np.maximum(new[:, M], F32(clip))
+    return new
+
+
+def _check_selection(name, got, samples, M, n):
+    ref = bc.select_top(samples, M, n)
+    keys = np.abs(samples[:, :M]).astype(F64)
+    for s in range(samples.shape[0]):
+        if not np.array_equal(got[s], ref[s]):
+            elite_equal(f"{name}[{s}]", got[s], ref[s], keys[s], tol=1e-6)
+
+
+def _run_mother(native, n, B, H, O, noise, seed):
+    ora, nat, xo, yo = make_pair(native, "mmd_opt", noise, n=n, O=O, H=H, B=B, T=2, acc_c=0.05, steer_c=0.01)
+    draws = oracle.Draws.random(ora.prob, np.random.default_rng(seed), idx_mpc=11, seed=0, with_beta_cem=True)
+    nat.begin("mmd_opt", 11, DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, xo, yo, 15.0, draws)
+    st = ora.init_state(DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, draws)
+    nat.run_stage(1, 0)
+    nat.run_stage(4, 0)
+    acc = nat.read("acc").reshape(B, 100)
+    steer = nat.read("steer").reshape(B, 100)
+    return ora, nat, xo, yo, draws, st, acc, steer
+
+
+@pytest.mark.parametrize("noise", ["gaussian", "beta"])
+def test_mother_features(native, noise):
+    n, B, H, O = 6, 24, 12, 3
+    ora, nat, xo, yo, draws, st, acc, steer = _run_mother(native, n, B, H, O, noise, 1)
+    p = ora.prob
+    acc_n, steer_n = Hh.noisy_controls(p, acc[:, :H], steer[:, :H], draws, 0, n)
+    ctrl = nat.read("ctrl_n").reshape(B, 2, n, H)
+    frac = 0.05 if noise == "beta" else 0.0
+    close("acc_n", ctrl[:, 0], acc_n, atol=1e-5, frac_ok=frac)
+    close("steer_n", ctrl[:, 1], steer_n, atol=1e-6, frac_ok=frac)
+    # features from the GPU's noisy rows (isolates the rollout + fit)
+    acc_m, steer_m = Hh.mother_controls(ctrl[:, 0], ctrl[:, 1])
+    xm, ym = Hh.rollout(p, acc_m, steer_m, st["st0"])
+    cxm, cym = Hh.compute_coeff(p, xm, ym)
+    feat = nat.read("feat").reshape(B, 22, n * n)
+    close("feat_cx", feat[:, :11].transpose(0, 2, 1), cxm, rtol=1e-4, atol=2e-4)
+    close("feat_cy", feat[:, 11:].transpose(0, 2, 1), cym, rtol=1e-4, atol=2e-4)
+
+
+@pytest.mark.parametrize("n,B,check", [(5, 20, None), (12, 20, [0, 7, 19]), (22, 20, [0, 19])])
+def test_beta_cem_lockstep(native, n, B, check):
+    H, O = 10, 3
+    ora, nat, xo, yo, draws, st, acc, steer = _run_mother(native, n, B, H, O, "gaussian", 2)
+    p = ora.prob
+    M = n * n
+    M1 = M + 1
+    cand = list(range(B)) if check is None else check
+    feat = nat.read("feat").reshape(B, 22, M)
+    Fb = {b: np.ascontiguousarray(feat[b].T) for b in cand}        # [M, 22]
+    z0, z = draws.beta_z0, draws.beta_z
+    samples = {}
+    for b in cand:
+        s0 = (SQRT20 * z0.astype(F64)).astype(F32)
+        s0[:, M] = np.maximum(s0[:, M], F32(0.01))
+        samples[b] = s0
+    res_ref = {b: np.zeros(20, F32) for b in cand}
+    for tb in range(20):
+        nat.run_stage(5, tb)
+        bsel = nat.read("bsel", np.int32).reshape(B, 100, n)
+        bsig = nat.read("bsig").reshape(B, 100)
+        for b in cand:
+            _check_selection(f"bsel[tb={tb},b={b}]", bsel[b], samples[b], M, n)
+            close(f"bsig[{tb},{b}]", bsig[b], samples[b][:, M], rtol=1e-6, atol=0)
+        nat.run_stage(6, tb)
+        btop = nat.read("btop").reshape(B, 100, n)
+        bcost = nat.read("bcost").reshape(B, 100)
+        for b in cand:
+            beta, cost, _, _ = bc.reduced_qp(p, Fb[b], bsel[b].astype(np.int64), bsig[b], M)
+            close(f"btop[{tb},{b}]", btop[b], beta, rtol=1e-3, atol=1e-4)
+            close(f"bcost[{tb},{b}]", bcost[b], cost, rtol=1e-4, atol=1e-4)
+        nat.run_stage(7, tb)
+        bel = nat.read("belite").reshape(2, B, 11, M1)[(tb + 1) & 1]
+        res_beta = nat.read("res_beta").reshape(B, 20)
+        for b in cand:
+            idx_e = Hh.argsort_stable(bcost[b])[:11]
+            close(f"elites[{tb},{b}]", bel[b], samples[b][idx_e], rtol=1e-6, atol=1e-6)
+            assert res_beta[b, tb] == np.min(bcost[b])
+            nxt = np.vstack([bel[b], _samples_from_elites(bel[b], z[tb], M)]).astype(F32)
+            if tb == 19:
+                imin = bc.argmin_nan(bcost[b])
+                beta_g = nat.read("beta").reshape(B, n)[b]
+                sel_g = nat.read("bestsel", np.int32).reshape(B, n)[b]
+                sig_g = nat.read("sigma")[b]
+                assert np.array_equal(sel_g, bsel[b, imin])
+                assert np.array_equal(beta_g, btop[b, imin])
+                close(f"sigma_best[{b}]", sig_g, nxt[imin, M], rtol=1e-6, atol=0)
+            samples[b] = nxt
+    # final reduced-set MMD on the GPU's beta-CEM outputs
+    nat.run_stage(8, 0)
+    ctrl = nat.read("ctrl_n").reshape(B, 2, n, H)
+    sel = nat.read("bestsel", np.int32).reshape(B, n)
+    beta = nat.read("beta").reshape(B, n)
+    sigma = nat.read("sigma")[:B]
+    acc_m, steer_m = Hh.mother_controls(ctrl[:, 0], ctrl[:, 1])
+    acc_r = np.take_along_axis(acc_m, sel[:, :, None].astype(np.int64), axis=1)
+    steer_r = np.take_along_axis(steer_m, sel[:, :, None].astype(np.int64), axis=1)
+    xr, yr = Hh.rollout(p, acc_r, steer_r, st["st0"])
+    cb = C.compute_f_bar_max(p, xr, yr, xo[:, :H], yo[:, :H])
+    obs = C.mmd(p, beta, cb, sigma)
+    lane = C.mmd_lane(p, beta, sigma, yr)
+    close("mmd_obs", nat.read("obs_cost")[:B], obs, rtol=1e-4, atol=1e-2)
+    close("mmd_lane", nat.read("lane_cost")[:B], lane, rtol=1e-4, atol=1e-2)
+
+
+def test_mmdopt_iteration(native):
+    """Full GPU iterations (noise, front, mother, 20 x beta-CEM, final MMD,
+    select) against the oracle iteration on the GPU's carry.  The beta-CEM
+    makes 2000 QP-cost comparisons per candidate; costs agree to ~1e-6
+    relative, so an elite flip inside it (and a different beta / sigma) is
+    possible but rare: obs costs must agree for >= 90% of candidates."""
+    from test_gpu_parity_baseline import _sync_state
+    n, B, H, O, Tf = 5, 24, 10, 3, 2
+    ora, nat, xo, yo = make_pair(native, "mmd_opt", "gaussian", n=n, O=O, H=H, B=B, T=Tf)
+    draws = oracle.Draws.random(ora.prob, np.random.default_rng(4), idx_mpc=3, with_beta_cem=True)
+    nat.begin("mmd_opt", 3, DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, xo, yo, 15.0, draws)
+    st = ora.init_state(DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, draws)
+    for t in range(Tf):
+        _sync_state(nat, st, B)
+        st["pop"] = nat.read("pop")[(t & 1) * B * 8:(t & 1) * B * 8 + B * 8].reshape(B, 8).copy()
+        ora.iteration("mmd_opt", st, t, xo, yo, np.float32(15.0), draws, trace := [])
+        tr = trace[0]
+        nat.iterate(t, 1)
+        nat.sync()
+        close(f"obs[{t}]", nat.read("obs_cost")[:B], tr["obs"], rtol=1e-3, atol=1e-2, frac_ok=0.1)
+        close(f"res_norm[{t}]", nat.read("res_norm")[:B], tr["res_norm"], atol=1e-5)
