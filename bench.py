@@ -1,0 +1,262 @@
+#!/usr/bin/env python3
+"""Throughput bench of the CEM-projection optimizer hot path (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload mmd_opt|cvar]
+
+One step = one outer CEM iteration (cem.py:221-315 body: initial guess,
+projection, controls, noisy rollouts, risk reducer (beta-CEM for mmd_opt),
+elite sorts, CEM update) over the whole batch, on device-resident inputs, with
+the library's internal Philox noise.  Every 20 steps a new solve starts
+(mpcmmd_begin: boundary vectors, initial population, obstacle upload), as in
+the reference's 20-iteration compute_cem_* call; that host work is inside the
+timed region.
+
+N > 1: one process per GPU (torchrun).  Each rank solves its own obstacle
+configuration (config k = rank, seeded like S/main_mpc.py:12,114), so per-GPU
+work is fixed ("scaling": "weak"); RCCL is used for the barrier, the max of
+the elapsed times and the final gather of the per-config results (§8e).
+
+Extra fields: "roofline" for the dominant kernel (HIP-event durations of the
+library's launches on its stream, during a profiled pass of the same steps)
+and "cpu_baseline" (the NumPy oracle on a bounded sample of the same
+workload, rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "mpc-mmd_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "MPC optimizer steps/s (batch=1024,H=30,obs_samp=500) @1/2/4/8 GPU; % HBM roofline"
+
+# BASELINE.json configs[1] (headline) and configs[2]
+WORKLOADS = {
+    "mmd_opt": dict(desc="static obs, mmd_opt, batch=1024 rollouts, H=30, num_obs=10, obs_samples=484 (n=22, M=n^2)",
+                    cost="mmd_opt", num_reduced=22, num_obs=10, num_prime=30, noise="gaussian", level=0.1,
+                    num_batch=1024),
+    "cvar": dict(desc="static obs, cvar, batch=1024 rollouts, H=30, num_obs=10, obs_samples=500, beta noise 0.3",
+                 cost="cvar", num_reduced=500, num_obs=10, num_prime=30, noise="beta", level=0.3,
+                 num_batch=1024),
+}
+
+FP32_PEAK_TFLOPS = 157.3   # MI355X fp32 vector (= fp32 MFMA) peak, MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+
+
+def kernel_work(w, name):
+    """Algorithmic work of ONE launch of kernel `name` (Kernels).
+    Returns (kind, amount): kind "flop" (fp32/fp64 VALU ops, exp = 1) or
+    "byte" (HBM bytes)."""
+    B, H, O = w["num_batch"], w["num_prime"], w["num_obs"]
+    n = w["num_reduced"]
+    M = n * n
+    if name == "bkernel":
+        # per candidate and beta-iteration: every distinct mother row's L1
+        # distances to all M rows (22 features, sub + abs-add = 2 flop) with
+        # the distinct-row count bounded by M, and for each of the 100 x n
+        # (sample, reduced row) pairs M Laplace terms (div 3, exp 2, add 1)
+        return "flop", B * (M * M * 22 * 2 + 100 * n * M * 6)
+    if name == "risk_baseline":
+        S = n
+        per_rollout_step = 40 + O * 9          # bicycle step (4 transcendentals) + f_bar per obstacle
+        beta = 2 * 160 if w["noise"] == "beta" else 0
+        return "flop", B * S * H * (per_rollout_step + beta)
+    if name == "mother":
+        return "flop", B * M * H * (40 + 44)    # bicycle step + fp64 fit accumulation (22 FMA)
+    if name == "bsample":
+        return "flop", B * (89 * (M + 1) * 2 * 11 * 2 + 100 * M * 4)
+    if name == "belite":
+        return "flop", B * ((M + 1) * (11 * 11 * 3 + 11 * 11 * 2 + 60))
+    return "flop", 0
+
+
+def make_workload(w, rank):
+    """Obstacle configuration k = rank: x without replacement from the
+    extended grid {35, 40, ...}, y in {-1.75, 1.75} (S/main_mpc.py:10-21,
+    SURVEY §8d), then idx_mpc = randint(1, 10000) (S/main_mpc.py:114)."""
+    from optimizer.cem_helper import Helper  # noqa: F401  (drop-in package import check)
+    O = w["num_obs"]
+    rs = np.random.RandomState(rank)
+    xs = np.arange(35, 35 + 5 * max(9, O), 5, dtype=np.float64)
+    x = rs.choice(xs, O, replace=False)
+    y = rs.choice(np.array([-1.75, 1.75]), O)
+    idx_mpc = int(rs.randint(1, 10000))
+    # static obstacles: constant position over the 100-point plan (cem_helper.py:366-378 with v = 0)
+    xo = np.repeat(x[:, None], 100, axis=1).astype(np.float32)
+    yo = np.repeat(y[:, None], 100, axis=1).astype(np.float32)
+    init = np.array([0.0, 1.75, 5.0, 0.0, 0.0, 0.0], np.float32)          # S/main_mpc.py:46-54
+    mean = np.array([15] * 4 + [0] * 4, np.float32)                       # S/main_mpc.py:58-71
+    cov = np.diag([20.0] * 4 + [100.0] * 4).astype(np.float32)
+    return dict(idx_mpc=idx_mpc, init=init, mean=mean, cov=cov, xo=xo, yo=yo, v_des=15.0)
+
+
+def cpu_baseline(w, inst, seconds):
+    """NumPy oracle (the CPU restatement of the reference) on a bounded sample
+    of one step of the same workload: the batch-wide stages (guess +
+    projection + controls, elite sorts + CEM update) on all B candidates and
+    the per-candidate risk stage on the first c candidates, scaled to B."""
+    import oracle
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([d.get("num_threads", 1) for d in threadpool_info()] + [1])
+    except Exception:
+        threads = 1
+    B = w["num_batch"]
+    ora = oracle.CEM(w["num_reduced"], w["num_obs"], w["level"], w["num_prime"], w["noise"], 0.0, 0.0,
+                     num_batch=B, maxiter_cem=1)
+    draws = oracle.Draws.philox(ora.prob, inst["idx_mpc"], seed=0, with_beta_cem=(w["cost"] == "mmd_opt"))
+    st = ora.init_state(inst["init"], inst["mean"], inst["cov"], draws)
+    t0 = time.perf_counter()
+    pr, acc, steer = ora.front(st)
+    t_front = time.perf_counter() - t0
+    # risk on growing candidate counts until the time budget is spent
+    c, t_risk = 0, 0.0
+    obs = np.zeros(B, np.float32)
+    lane = np.zeros(B, np.float32)
+    while c < B and t_risk < seconds:
+        step = 1 if w["cost"] == "mmd_opt" else min(B - c, 64)
+        t0 = time.perf_counter()
+        o, l, _ = ora.candidate_costs(w["cost"], st, acc[c:c + step], steer[c:c + step], inst["xo"], inst["yo"],
+                                      draws, 0)
+        t_risk += time.perf_counter() - t0
+        obs[c:c + step], lane[c:c + step] = o, l
+        c += step
+    t0 = time.perf_counter()
+    n = w["num_reduced"]
+    extra = dict(beta=np.full((B, n), np.float32(1.0 / n)), sigma=np.full(B, np.float32(0.01)),
+                 res_beta=np.zeros((B, 20), np.float32))
+    ora.select(w["cost"], st, 0, pr, steer, obs, lane, np.float32(inst["v_des"]), draws, extra)
+    t_select = time.perf_counter() - t0
+    t_step = t_front + t_risk * (B / c) + t_select
+    return {"value": 1.0 / t_step, "unit": "steps/s", "cores": int(threads), "kind": "port",
+            "sample": (f"oracle (NumPy restatement of the reference) one CEM step: front+select on all {B} "
+                       f"candidates ({t_front + t_select:.2f} s), risk stage on {c} of {B} candidates "
+                       f"({t_risk:.1f} s) scaled x{B / c:.1f}; BLAS threads {threads}")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="mmd_opt", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--profile-steps", type=int, default=20)
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from optimizer import _native
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world} (launch N>1 with torchrun)")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    w = WORKLOADS[a.workload]
+    inst = make_workload(w, rank)
+    T = 20
+    cfg = _native.make_config(w["num_reduced"], w["num_obs"], w["level"], w["num_prime"], w["noise"], 0.0, 0.0,
+                              num_batch=w["num_batch"], maxiter_cem=T, device=local, seed=rank)
+    h = _native.Handle(cfg)
+    stream = torch.cuda.current_stream()
+    h.set_stream(stream.cuda_stream)
+
+    def run(k0, count):
+        for i in range(k0, k0 + count):
+            t = i % T
+            if t == 0:
+                h.begin(w["cost"], inst["idx_mpc"], inst["init"], inst["mean"], inst["cov"], inst["xo"], inst["yo"],
+                        inst["v_des"])
+            h.iterate(t, 1)
+
+    run(0, a.warmup)
+    h.sync()
+    torch.cuda.synchronize()
+    # timed region: K steps, fresh solve boundaries every 20 steps
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    run(0, a.steps)
+    ev1.record(stream)
+    h.sync()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ev_ms = ev0.elapsed_time(ev1)
+    if world > 1:
+        el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        elapsed = float(el.item())
+        dist.barrier()
+    res = h.finish()
+    # profiled pass (same steps, HIP events around every launch on the library's stream)
+    h.profile(True)
+    run(0, a.profile_steps)
+    h.sync()
+    kt = h.kernel_times()
+    h.profile(False)
+    # final gather of per-config results over RCCL (§8e)
+    vec = np.concatenate([res["cx"], res["cy"], [res["cost_lane"], res["cost_obs"]]]).astype(np.float32)
+    if world > 1:
+        vt = torch.from_numpy(vec).cuda()
+        allv = [torch.empty_like(vt) for _ in range(world)]
+        dist.all_gather(allv, vt)
+        gathered = torch.stack(allv).cpu().numpy()
+    else:
+        gathered = vec[None]
+    if rank == 0:
+        steps_total = a.steps * world
+        value = steps_total / elapsed
+        busy = {k: v for k, v in kt.items() if v[0] > 0}
+        dom = max(busy, key=lambda k: busy[k][1])
+        launches, tot_ms = busy[dom]
+        avg_s = tot_ms / launches / 1e3
+        kind, amount = kernel_work(w, dom)
+        if kind == "byte":
+            roof = {"bound": "hbm", "achieved": amount / avg_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+        else:
+            roof = {"bound": "valu", "achieved": amount / avg_s / 1e12, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s"}
+        roof["frac"] = roof["achieved"] / roof["peak"]
+        roof["traffic"] = None
+        roof["kernel"] = dom
+        roof["avg_us"] = avg_s * 1e6
+        line = {
+            "metric": METRIC, "value": value, "unit": "steps/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (static obstacle configs k=rank, internal Philox noise)",
+            "config": {"workload": w["desc"], "cost": w["cost"], "global_batch": w["num_batch"] * world,
+                       "num_batch": w["num_batch"], "num_prime": w["num_prime"], "num_obs": w["num_obs"],
+                       "num_reduced": w["num_reduced"], "noise": w["noise"], "noise_level": w["level"],
+                       "parallelism": f"config-sharded x{world}", "solves_per_s": value / T},
+            "roofline": roof,
+            "kernels_ms_per_step": {k: v[1] / a.profile_steps for k, v in busy.items()},
+            "event_ms_rank0": ev_ms,
+            "results_gathered": int(gathered.shape[0]),
+        }
+        if world == 1 and a.cpu_seconds > 0:
+            line["cpu_baseline"] = cpu_baseline(w, inst, a.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    h.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
