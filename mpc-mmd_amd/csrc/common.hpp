@@ -11,6 +11,14 @@
 
 namespace mpcmmd {
 
+// phase timestamp of workgroup 0 into dbg[slot] (profiling only)
+#define MPCMMD_STAMP(p, slot)                                                   \
+  do {                                                                          \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (p).dbg)                         \
+      (p).dbg[(slot)] = __builtin_amdgcn_s_memrealtime();                       \
+  } while (0)
+
+
 constexpr int kWave = 64;
 
 // ---- wave-wide reductions (result valid in every lane) ----------------------

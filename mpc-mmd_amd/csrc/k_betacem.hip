@@ -36,11 +36,19 @@ namespace {
 constexpr int kF = 22;                               // features: cx (11) | cy (11)
 constexpr int kNew = kBetaSamples - kBetaElite;      // 89 resampled rows per iteration
 constexpr int kThreads = 512;
-constexpr int kMaxQ = 16;                            // M <= 1024 -> 16 values per lane
 constexpr double kSqrt20 = 4.47213595499957927704;   // chol(20 I) (compute_beta.py:24)
 constexpr double kRidge = 0.05;                      // cov jitter (compute_beta.py:61)
+constexpr double kInvRidge = 20.0;
 
-DEVI void wave_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+#define kconst __attribute__((address_space(4)))
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// Intra-wave LDS hand-off: a wave's LDS operations execute in order, so only
+// the compiler must be kept from reordering them (no memory-counter waits).
+DEVI void wave_sync() {
+  __builtin_amdgcn_wave_barrier();
+  __asm__ volatile("" ::: "memory");
+}
 
 // ------------------------------------------------------------------------
 // k_mother
@@ -91,47 +99,79 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
 // ------------------------------------------------------------------------
 // top-n of |v_j| (j < M) in jnp.argsort order, one wave.  out[k] (k < n) are
 // the indices at sorted positions M-n+k (ascending by (|v|, j)).
+// Lane holds NQ keys (j = lane + 64 q).  The n-th largest key is found by
+// bisection on the key bits with ballot counts; the search stops as soon as
+// exactly n keys lie above the candidate threshold (continuous data: ~10 of
+// the 31 steps).  Ties at the threshold go to the largest indices.
 // scratch: 2 * 32 ints of LDS owned by the wave.
-template <class V>
-DEVI void select_top(V val, int M, int n, int32_t* out, int* scratch) {
+template <int NQ, class V>
+DEVI void load_keys(V val, int M, uint32_t* key) {
   const int lane = threadIdx.x & 63;
-  const int nq = (M + 63) >> 6;
-  uint32_t key[kMaxQ];
 #pragma unroll
-  for (int q = 0; q < kMaxQ; ++q) {
+  for (int q = 0; q < NQ; ++q) {
     const int j = lane + 64 * q;
-    key[q] = (q < nq && j < M) ? sort_key(fabsf(val(j))) : 0u;
+    key[q] = j < M ? sort_key(fabsf(val(j))) : 0u;  // real keys have bit 31 set
   }
-  // T = n-th largest key (bisection on the key bits)
-  uint32_t T = 0u;
-  for (int bit = 31; bit >= 0; --bit) {
-    const uint32_t cand = T | (1u << bit);
-    int cnt = 0;
+}
+
+// Threshold search for NB samples at once (independent chains interleave):
+// T[u] = the n-th largest key of sample u, or exact[u] when exactly n keys
+// are >= T[u] (the search stops early for continuous data).
+template <int NQ, int NB>
+DEVI void find_thresholds(const uint32_t (*key)[NQ], int nb, int n, uint32_t* T, bool* exact) {
 #pragma unroll
-    for (int q = 0; q < kMaxQ; ++q)
-      if (q < nq) cnt += __popcll(__ballot(key[q] >= cand));
-    if (cnt >= n) T = cand;
+  for (int u = 0; u < NB; ++u) {
+    T[u] = 0x80000000u;  // real keys have bit 31 set, padding keys are 0
+    exact[u] = u >= nb;
   }
-  int gt = 0;
+  for (int bit = 30; bit >= 0; --bit) {
+    bool all = true;
 #pragma unroll
-  for (int q = 0; q < kMaxQ; ++q)
-    if (q < nq) gt += __popcll(__ballot(key[q] > T));
-  const int need = n - gt;  // equal keys taken from the largest indices
-  unsigned long long eqm[kMaxQ];
+    for (int u = 0; u < NB; ++u) {
+      if (exact[u]) continue;
+      const uint32_t cand = T[u] | (1u << bit);
+      int cnt = 0;
 #pragma unroll
-  for (int q = 0; q < kMaxQ; ++q) eqm[q] = q < nq ? __ballot(key[q] == T) : 0ull;
+      for (int q = 0; q < NQ; ++q) cnt += __popcll(__ballot(key[u][q] >= cand));
+      if (cnt >= n) T[u] = cand;
+      exact[u] = cnt == n;
+      all = all && exact[u];
+    }
+    if (all) break;
+  }
+}
+
+// Given the threshold, write the indices of the top n keys to out[0..n) in
+// jnp.argsort order (ascending key, ties by index).  Ties at a non-exact
+// threshold go to the largest indices.
+template <int NQ>
+DEVI void emit_top(const uint32_t* key, uint32_t T, bool exact, int n, int32_t* out, int* scratch) {
+  const int lane = threadIdx.x & 63;
+  int need = 0;
+  unsigned long long eqm[NQ];
+  if (!exact) {
+    int gt = 0;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) gt += __popcll(__ballot(key[q] > T));
+    need = n - gt;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) eqm[q] = __ballot(key[q] == T);
+  } else {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) eqm[q] = 0ull;
+  }
   const unsigned long long above = lane == 63 ? 0ull : (~0ull << (lane + 1));
   int* lj = scratch;
   uint32_t* lk = reinterpret_cast<uint32_t*>(scratch + 32);
   int base = 0;
   int later_eq = 0;  // equal keys in q' > q
-  for (int q = nq - 1; q >= 0; --q) later_eq += __popcll(eqm[q]);
 #pragma unroll
-  for (int q = 0; q < kMaxQ; ++q) {
-    if (q >= nq) break;
+  for (int q = 0; q < NQ; ++q) later_eq += __popcll(eqm[q]);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
     later_eq -= __popcll(eqm[q]);
     const int larger = later_eq + __popcll(eqm[q] & above);
-    const bool sel = key[q] > T || (key[q] == T && larger < need);
+    const bool sel = exact ? key[q] >= T : (key[q] > T || (key[q] == T && larger < need));
     const unsigned long long sm = __ballot(sel);
     if (sel) {
       const int pos = base + __popcll(sm & ((1ull << lane) - 1ull));
@@ -141,126 +181,242 @@ DEVI void select_top(V val, int M, int n, int32_t* out, int* scratch) {
     base += __popcll(sm);
   }
   wave_sync();
-  if (lane < n) {
-    const int j = lj[lane];
-    const uint32_t k = lk[lane];
-    int r = 0;
-    for (int c = 0; c < n; ++c) {
-      const uint32_t kc = lk[c];
-      const int jc = lj[c];
-      r += (kc < k) || (kc == k && jc < j);
-    }
-    out[r] = j;
+  // compaction order is ascending index, so ties rank by lane
+  const int j = lane < n ? lj[lane] : 0;
+  const uint32_t k = lane < n ? lk[lane] : 0xFFFFFFFFu;
+  int r = 0;
+  for (int c = 0; c < n; ++c) {
+    const uint32_t kc = __builtin_amdgcn_readlane(k, c);
+    r += (kc < k) || (kc == k && c < lane);
   }
+  if (lane < n) out[r] = j;
   wave_sync();
 }
 
-// ------------------------------------------------------------------------
-// New beta-CEM samples with the structured Cholesky (see file header).
-// lanes = samples (sidx(lane) = new-sample index 0..88, or -1), waves =
-// position blocks; two passes: block partial sums P = sum w_j z_j, then the
-// scan.  emit(lane, j, y) receives fp32 y for every position j <= M.
-// Pbuf: 8 * 11 * 64 doubles of LDS (may alias the emit target: a barrier
-// separates its last read from the first emit).
-template <class SIdx, class Emit>
-DEVI void generate(const Params& p, int b, int tz, SIdx sidx, Emit emit, double* Pbuf) {
-  const int M1 = p.M + 1, lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int bs = (M1 + nw - 1) / nw;
-  const int j0 = min(M1, w * bs), j1 = min(M1, j0 + bs);
-  const double* G = p.gen + size_t(b) * M1 * kGenStride;
-  const float* gm = p.genm + size_t(b) * M1;
-  const float* z = p.beta_z + size_t(tz) * M1 * kNew;  // device layout [M+1][89]
-  const int si = sidx(lane);
-  const bool act = si >= 0;
-  const int sz = act ? si : 0;
-  double P[11];
+// Top-n selection for the samples s = first, first + stride, ... < last of
+// one wave, NB at a time: keys of NB samples are loaded together and their
+// threshold searches interleave.  row(s) -> values, out(s) -> int32[n].
+template <int NQ, class Row, class Out>
+DEVI void select_batch(Row row, Out out, int first, int last, int stride, int M, int n, int* scratch) {
+  constexpr int NB = NQ <= 8 ? 4 : (NQ <= 12 ? 2 : 1);
+  for (int s0 = first; s0 < last; s0 += NB * stride) {
+    uint32_t key[NB][NQ];
+    int nb = 0;
 #pragma unroll
-  for (int k = 0; k < 11; ++k) P[k] = 0.0;
-  for (int j = j0; j < j1; ++j) {
-    const double zj = act ? double(z[size_t(j) * kNew + sz]) : 0.0;
-    const double* g = G + size_t(j) * kGenStride;
+    for (int u = 0; u < NB; ++u) {
+      const int s = s0 + u * stride;
+      if (s < last) {
+        load_keys<NQ>(row(s), M, key[u]);
+        nb = u + 1;
+      }
+    }
+    uint32_t T[NB];
+    bool exact[NB];
+    find_thresholds<NQ, NB>(key, nb, n, T, exact);
 #pragma unroll
-    for (int k = 0; k < 11; ++k) P[k] = P[k] + g[k] * zj;
+    for (int u = 0; u < NB; ++u)
+      if (u < nb) emit_top<NQ>(key[u], T[u], exact[u], n, out(s0 + u * stride), scratch);
   }
-#pragma unroll
-  for (int k = 0; k < 11; ++k) Pbuf[(w * 11 + k) * 64 + lane] = P[k];
-  __syncthreads();
-  double S[11];
-#pragma unroll
-  for (int k = 0; k < 11; ++k) {
-    double c = 0.0;
-    for (int w2 = 0; w2 < w; ++w2) c = c + Pbuf[(w2 * 11 + k) * 64 + lane];
-    S[k] = c;
-  }
-  __syncthreads();
-  for (int j = j0; j < j1; ++j) {
-    const double zj = act ? double(z[size_t(j) * kNew + sz]) : 0.0;
-    const double* g = G + size_t(j) * kGenStride;
-    double d = 0.0;
-#pragma unroll
-    for (int k = 0; k < 11; ++k) d = d + g[11 + k] * S[k];
-    const double yv = (double(gm[j]) + g[22] * zj) + d;
-#pragma unroll
-    for (int k = 0; k < 11; ++k) S[k] = S[k] + g[k] * zj;
-    if (act) emit(lane, j, float(yv));
+}
+
+template <class Row, class Out>
+DEVI void select_rows(Row row, Out out, int first, int last, int stride, int M, int n, int* scratch) {
+  switch ((M + 63) >> 6) {
+#define MPCMMD_SEL_CASE(q) \
+  case q:                  \
+    return select_batch<q>(row, out, first, last, stride, M, n, scratch);
+    MPCMMD_SEL_CASE(1)
+    MPCMMD_SEL_CASE(2)
+    MPCMMD_SEL_CASE(3)
+    MPCMMD_SEL_CASE(4)
+    MPCMMD_SEL_CASE(5)
+    MPCMMD_SEL_CASE(6)
+    MPCMMD_SEL_CASE(7)
+    MPCMMD_SEL_CASE(8)
+    MPCMMD_SEL_CASE(9)
+    MPCMMD_SEL_CASE(10)
+    MPCMMD_SEL_CASE(11)
+    MPCMMD_SEL_CASE(12)
+    MPCMMD_SEL_CASE(13)
+    MPCMMD_SEL_CASE(14)
+    MPCMMD_SEL_CASE(15)
+#undef MPCMMD_SEL_CASE
+    default:
+      return select_batch<16>(row, out, first, last, stride, M, n, scratch);
   }
 }
 
 // ------------------------------------------------------------------------
 // k_bsample: the 100 samples of beta-CEM iteration tb and their top-n rows.
-__global__ __launch_bounds__(kThreads) void k_bsample(Params p, int tb, int spr) {
+//
+// New samples (rows 11..99) use the structured Cholesky (file header):
+// lanes = samples, waves = position blocks, two passes (block partial sums
+// P = sum_j w_j z_j, then the scan y_j = m_j + L_jj z_j + u_j . S_j).  The
+// candidate's generators (W, U, L_jj, m per position, 192 B) are staged in
+// LDS once, so the serial chain over positions is LDS-broadcast bound.  The
+// samples go to ygen (global, row per sample) for the selection and for
+// k_belite's elite copy.
+constexpr int kZChunk = 16;  // positions per register chunk of normals in the generation
+HDI size_t bs_gbytes(int M1) { return (size_t(M1) * kGenStride * 8 + 15) & ~size_t(15); }
+HDI size_t bs_pbytes() { return size_t(8) * 11 * 64 * 8; }
+HDI size_t bs_lds(int M1) { return bs_gbytes(M1) + bs_pbytes() + size_t(8) * 64 * 4; }
+
+__global__ __launch_bounds__(kThreads) void k_bsample(Params p, int tb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x, M = p.M, M1 = M + 1, n = p.n;
-  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
-  const int ys = spr + 1;
-  float* ybuf = reinterpret_cast<float*>(smem);
-  size_t ybytes = size_t(M1) * ys * 4;
-  const size_t pbytes = size_t(8) * 11 * 64 * 8;
-  if (ybytes < pbytes) ybytes = pbytes;
-  int* wscr = reinterpret_cast<int*>(smem + ((ybytes + 15) & ~size_t(15))) + w * 64;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+  double* Gl = reinterpret_cast<double*>(smem);
+  double* Pbuf = reinterpret_cast<double*>(smem + bs_gbytes(M1));
+  int* wscr = reinterpret_cast<int*>(smem + bs_gbytes(M1) + bs_pbytes()) + w * 64;
   int32_t* sel = p.bsel + size_t(b) * kBetaSamples * n;
   float* sig = p.bsig + size_t(b) * kBetaSamples;
+  MPCMMD_STAMP(p, 0);
   if (tb == 0) {
     // initial samples MVN(0, 20 I) with chol(20 I) = sqrt(20) I (compute_beta.py:41-49)
-    for (int s = w; s < kBetaSamples; s += nw) {
-      const float* z0 = p.beta_z0 + size_t(s) * M1;
-      auto val = [&](int j) { return float(kSqrt20 * double(z0[j])); };
-      select_top(val, M, n, sel + s * n, wscr);
-      if (lane == 0) sig[s] = fmaxf(val(M), 0.01f);
-    }
+    select_rows(
+        [&](int s) {
+          const float* z0 = p.beta_z0 + size_t(s) * M1;
+          return [=](int j) { return float(kSqrt20 * double(z0[j])); };
+        },
+        [&](int s) { return sel + s * n; }, w, kBetaSamples, nw, M, n, wscr);
+    if (threadIdx.x < kBetaSamples)
+      sig[threadIdx.x] = fmaxf(float(kSqrt20 * double(p.beta_z0[size_t(threadIdx.x) * M1 + M])), 0.01f);
     return;
+  }
+  // generators of iteration tb-1 -> LDS (W 0..10, U 11..21, L_jj 22, m 23)
+  const double* G = p.gen + size_t(b) * M1 * kGenStride;
+  const float* gm = p.genm + size_t(b) * M1;
+  for (int i = threadIdx.x; i < M1 * kGenStride; i += blockDim.x) {
+    const int j = i / kGenStride, k = i - j * kGenStride;
+    Gl[i] = k == 23 ? double(gm[j]) : G[i];
   }
   // rows 0..10: the previous iteration's elites (compute_beta.py:62)
   const float* E = p.belite + (size_t(tb & 1) * p.B + b) * kBetaElite * M1;
-  for (int s = w; s < kBetaElite; s += nw) {
-    const float* e = E + size_t(s) * M1;
-    auto val = [&](int j) { return e[j]; };
-    select_top(val, M, n, sel + s * n, wscr);
-    if (lane == 0) sig[s] = e[M];
-  }
-  // rows 11..99: mean + L z (compute_beta.py:63), in rounds of spr samples
-  for (int r0 = 0; r0 < kNew; r0 += spr) {
-    const int ns = min(spr, kNew - r0);
-    __syncthreads();
-    generate(
-        p, b, tb - 1, [&](int l) { return l < ns ? r0 + l : -1; },
-        [&](int l, int j, float y) { ybuf[size_t(j) * ys + l] = y; }, reinterpret_cast<double*>(smem));
-    __syncthreads();
-    for (int sl = w; sl < ns; sl += nw) {
-      auto val = [&](int j) { return ybuf[size_t(j) * ys + sl]; };
-      const int s = kBetaElite + r0 + sl;
-      select_top(val, M, n, sel + s * n, wscr);
-      if (lane == 0) sig[s] = fmaxf(val(M), 0.01f);
+  select_rows(
+      [&](int s) {
+        const float* e = E + size_t(s) * M1;
+        return [=](int j) { return e[j]; };
+      },
+      [&](int s) { return sel + s * n; }, w, kBetaElite, nw, M, n, wscr);
+  if (threadIdx.x < kBetaElite) sig[threadIdx.x] = E[size_t(threadIdx.x) * M1 + M];
+  __syncthreads();
+  MPCMMD_STAMP(p, 1);
+  // rows 11..99: mean + L z (compute_beta.py:63), 64 samples per round
+  const float* z = p.beta_z + size_t(tb - 1) * M1 * kNew;  // device layout [M+1][89]
+  const int ys = ygen_stride(M);
+  float* Y = p.ygen + size_t(b) * kNew * ys;
+  const int bs = (M1 + nw - 1) / nw;
+  const int j0 = min(M1, w * bs), j1 = min(M1, j0 + bs);
+  for (int r0 = 0; r0 < kNew; r0 += 64) {
+    const int ns = min(64, kNew - r0);
+    const bool act = lane < ns;
+    const int sz = r0 + (act ? lane : 0);
+    // standard normals of this wave's positions, register double-buffered in
+    // chunks of 16 positions (the next chunk's loads fly during the FMAs)
+    auto load = [&](float* zc, int c0) {
+#pragma unroll
+      for (int q = 0; q < kZChunk; ++q) {
+        const int j = c0 + q;
+        zc[q] = j < j1 ? z[size_t(j) * kNew + sz] : 0.0f;
+      }
+    };
+    double P[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) P[k] = 0.0;
+    auto passA = [&](const float* zc, int c0) {
+#pragma unroll
+      for (int q = 0; q < kZChunk; ++q) {
+        if (c0 + q >= j1) break;
+        const double zj = double(zc[q]);
+        const double* g = Gl + (c0 + q) * kGenStride;
+#pragma unroll
+        for (int k = 0; k < 11; ++k) P[k] = fma(g[k], zj, P[k]);
+      }
+    };
+    float za[kZChunk], zb[kZChunk];
+    load(za, j0);
+    for (int c0 = j0; c0 < j1; c0 += 2 * kZChunk) {
+      load(zb, c0 + kZChunk);
+      passA(za, c0);
+      load(za, c0 + 2 * kZChunk);
+      passA(zb, c0 + kZChunk);
     }
+#pragma unroll
+    for (int k = 0; k < 11; ++k) Pbuf[(w * 11 + k) * 64 + lane] = P[k];
+    __syncthreads();
+    double S[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) {
+      double c = 0.0;
+      for (int w2 = 0; w2 < w; ++w2) c = c + Pbuf[(w2 * 11 + k) * 64 + lane];
+      S[k] = c;
+    }
+    float* yrow = Y + size_t(sz) * ys;
+    auto passB = [&](const float* zc, int c0) {
+#pragma unroll
+      for (int q = 0; q < kZChunk; ++q) {
+        const int j = c0 + q;
+        if (j >= j1) break;
+        const double zj = double(zc[q]);
+        const double* g = Gl + j * kGenStride;
+        double d = 0.0;
+#pragma unroll
+        for (int k = 0; k < 11; ++k) d = fma(g[11 + k], S[k], d);
+        const double yv = fma(g[22], zj, g[23]) + d;
+#pragma unroll
+        for (int k = 0; k < 11; ++k) S[k] = fma(g[k], zj, S[k]);
+        if (act) yrow[j] = j == M ? fmaxf(float(yv), 0.01f) : float(yv);
+      }
+    };
+    load(za, j0);
+    for (int c0 = j0; c0 < j1; c0 += 2 * kZChunk) {
+      load(zb, c0 + kZChunk);
+      passB(za, c0);
+      load(za, c0 + 2 * kZChunk);
+      passB(zb, c0 + kZChunk);
+    }
+    __syncthreads();
+    MPCMMD_STAMP(p, 2 + 2 * (r0 >> 6));
+    select_rows(
+        [&](int sl) {
+          const float* y = Y + size_t(r0 + sl) * ys;
+          return [=](int j) { return y[j]; };
+        },
+        [&](int sl) { return sel + (kBetaElite + r0 + sl) * n; }, w, ns, nw, M, n, wscr);
+    if (threadIdx.x < ns) sig[kBetaElite + r0 + threadIdx.x] = Y[size_t(r0 + threadIdx.x) * ys + M];
+    MPCMMD_STAMP(p, 3 + 2 * (r0 >> 6));
   }
+  __syncthreads();
+  MPCMMD_STAMP(p, 15);
 }
 
 // ------------------------------------------------------------------------
-// k_bkernel LDS carve (host and device agree)
+// k_bkernel: one workgroup (1024 threads) per candidate.
+//
+//   rows     the distinct mother rows any sample selected (union, ~150 of 484
+//            on average; every K_mixed row is a row of the M x M mother
+//            distance matrix, kernel_computation.py:33-39)
+//   D chunk  rows of the L1 distance matrix in LDS, register-tiled: a thread
+//            owns one column j (its 22 features in registers) and walks the
+//            chunk's rows, whose features are LDS broadcasts
+//   pairs    (sample, reduced row) pairs sorted by row; a 16-lane group sums
+//            exp(-D[r][j] / sigma_s) over j (v_exp_f32 on d * (-log2 e / sigma))
+//   QP       2 samples per wave, lane = row: K_red (strict lower triangle
+//            spread over the half-wave), left-looking fp64 Cholesky of
+//            C = K_red + 0.05 I with the lane's row in registers, two
+//            triangular solves (g and 1), beta = x1 + ((1 - sum x1)/sum x2) x2,
+//            cost = beta^T K beta - 2 g^T beta with beta^T C beta = |L^T beta|^2
+constexpr int kKerThreads = 1024;
+constexpr int kFr = 24;  // row-major feature stride (floats): 22 + pad for b128 reads
+
 struct KerLds {
-  size_t F, sel, rsig, rowsum, cnt, start, fill, ulist, urank, pairs, work, total;
+  size_t Fr, sel, csg, rowsum, cnt, start, fill, ulist, urank, pairs, work, total;
   int rows;  // D-chunk rows
 };
+
+// per half-wave: packed lower triangle (n(n+1)/2 doubles) + 1/L_jj (32 doubles)
+HDI size_t ker_qp_slot(int n) { return size_t(n) * (n + 1) / 2 + 32; }
+HDI size_t ker_qp_bytes(int n) { return size_t(kKerThreads / 64) * 2 * ker_qp_slot(n) * 8; }
 
 HDI KerLds ker_lds(int M, int n, size_t budget) {
   KerLds L{};
@@ -270,9 +426,9 @@ HDI KerLds ker_lds(int M, int n, size_t budget) {
     o = (o + bytes + 15) & ~size_t(15);
     return at;
   };
-  L.F = take(size_t(kF) * M * 4);
+  L.Fr = take(size_t(M) * kFr * 4);
   L.sel = take(size_t(kBetaSamples) * n * 2);
-  L.rsig = take(size_t(2) * kBetaSamples * 4);
+  L.csg = take(size_t(kBetaSamples) * 4);
   L.rowsum = take(size_t(kBetaSamples) * n * 8);
   L.cnt = take(size_t(M) * 4);
   L.start = take(size_t(M) * 4);
@@ -281,29 +437,61 @@ HDI KerLds ker_lds(int M, int n, size_t budget) {
   L.urank = take(size_t(M) * 4);
   L.pairs = take(size_t(kBetaSamples) * n * 2);
   L.work = o;
-  // QP needs per wave: packed L (n(n+1)/2 doubles) + K [32][33] floats + beta [32] doubles
-  const size_t qp = size_t(8) * ((size_t(n) * (n + 1) / 2) * 8 + 32 * 33 * 4 + 32 * 8 + 64);
-  size_t rest = budget > o ? budget - o : 0;
-  int rows = int(rest / (size_t(M) * 4));
-  if (rows > 64) rows = 64;
+  const size_t rest = budget > o ? budget - o : 0;
+  const int Ms = (M + 1) & ~1;  // even row stride: float2 reads
+  int rows = int(rest / (size_t(Ms) * 4));
+  if (rows > 128) rows = 128;
   L.rows = rows;
-  size_t work = size_t(rows) * M * 4;
+  size_t work = size_t(rows) * Ms * 4;
+  const size_t qp = ker_qp_bytes(n);
   if (work < qp) work = qp;
   L.total = o + work;
   return L;
 }
 
 constexpr size_t kLdsBudget = 160 * 1024 - 1024;
+constexpr float kNegLog2e = -1.44269504088896340736f;
 
-__global__ __launch_bounds__(kThreads) void k_bkernel(Params p, int tb) {
+// value of lane j of this half-wave (lanes 0..31 | 32..63), via readlane
+DEVI double bcast_half(double v, int j, int hw) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = int(bits), hi = int(bits >> 32);
+  const int l0 = __builtin_amdgcn_readlane(lo, j), h0 = __builtin_amdgcn_readlane(hi, j);
+  const int l1 = __builtin_amdgcn_readlane(lo, j + 32), h1 = __builtin_amdgcn_readlane(hi, j + 32);
+  const long long r0 = (static_cast<long long>(h0) << 32) | static_cast<unsigned>(l0);
+  const long long r1 = (static_cast<long long>(h1) << 32) | static_cast<unsigned>(l1);
+  return __longlong_as_double(hw ? r1 : r0);
+}
+
+// sum_f |a_f - b_f| over the 22 features, sequential (oracle l1_dist order)
+DEVI float l1_22(const float* a, const float* b) {
+  float d = fabsf(a[0] - b[0]);
+#pragma unroll
+  for (int f = 1; f < kF; ++f) d = d + fabsf(a[f] - b[f]);
+  return d;
+}
+
+DEVI void load_row(const float* Fr, int r, float* out) {
+  const float4* s = reinterpret_cast<const float4*>(Fr + r * kFr);
+#pragma unroll
+  for (int q = 0; q < kFr / 4; ++q) {
+    const float4 v = s[q];
+    out[4 * q] = v.x;
+    out[4 * q + 1] = v.y;
+    out[4 * q + 2] = v.z;
+    out[4 * q + 3] = v.w;
+  }
+}
+
+__global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x, M = p.M, n = p.n;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6), nw = kKerThreads >> 6;
   const KerLds C = ker_lds(M, n, kLdsBudget);
-  float* Fl = reinterpret_cast<float*>(smem + C.F);
+  float* Fr = reinterpret_cast<float*>(smem + C.Fr);
   short* sl = reinterpret_cast<short*>(smem + C.sel);
-  float* sg = reinterpret_cast<float*>(smem + C.rsig);
-  float* rsg = sg + kBetaSamples;
+  float* csg = reinterpret_cast<float*>(smem + C.csg);
   double* rowsum = reinterpret_cast<double*>(smem + C.rowsum);
   int* cnt = reinterpret_cast<int*>(smem + C.cnt);
   int* start = reinterpret_cast<int*>(smem + C.start);
@@ -313,22 +501,20 @@ __global__ __launch_bounds__(kThreads) void k_bkernel(Params p, int tb) {
   short* pairs = reinterpret_cast<short*>(smem + C.pairs);
   float* Dl = reinterpret_cast<float*>(smem + C.work);
   const float* Fg = p.feat + size_t(b) * kF * M;
-  for (int i = tid; i < kF * M; i += blockDim.x) Fl[i] = Fg[i];
-  const int32_t* sg_sel = p.bsel + size_t(b) * kBetaSamples * n;
-  for (int i = tid; i < kBetaSamples * n; i += blockDim.x) sl[i] = short(sg_sel[i]);
-  for (int s = tid; s < kBetaSamples; s += blockDim.x) {
-    const float v = p.bsig[size_t(b) * kBetaSamples + s];
-    sg[s] = v;
-    rsg[s] = 1.0f / v;
+  MPCMMD_STAMP(p, 16);
+  for (int i = tid; i < kFr * M; i += kKerThreads) {
+    const int j = i / kFr, f = i - j * kFr;
+    Fr[i] = f < kF ? Fg[size_t(f) * M + j] : 0.0f;
   }
-  for (int r = tid; r < M; r += blockDim.x) {
+  const int32_t* gsel = p.bsel + size_t(b) * kBetaSamples * n;
+  for (int i = tid; i < kBetaSamples * n; i += kKerThreads) sl[i] = short(gsel[i]);
+  for (int s = tid; s < kBetaSamples; s += kKerThreads) csg[s] = kNegLog2e / p.bsig[size_t(b) * kBetaSamples + s];
+  for (int r = tid; r < M; r += kKerThreads) {
     cnt[r] = 0;
     fill[r] = 0;
   }
   __syncthreads();
-  // ---- rows used by any sample (the reduced rows are mother rows, so every
-  // K_mixed row is a row of the M x M mother distance matrix)
-  for (int i = tid; i < kBetaSamples * n; i += blockDim.x) atomicAdd(&cnt[sl[i]], 1);
+  for (int i = tid; i < kBetaSamples * n; i += kKerThreads) atomicAdd(&cnt[sl[i]], 1);
   __syncthreads();
   if (w == 0) {  // exclusive scans of cnt and (cnt > 0), one wave
     const int per = (M + 63) / 64, a = lane * per, e = min(M, a + per);
@@ -357,37 +543,53 @@ __global__ __launch_bounds__(kThreads) void k_bkernel(Params p, int tb) {
   }
   __syncthreads();
   const int U = urank[M - 1] + (cnt[M - 1] > 0);
-  for (int i = tid; i < kBetaSamples * n; i += blockDim.x) {
+  for (int i = tid; i < kBetaSamples * n; i += kKerThreads) {
     const int r = sl[i];
     const int pos = start[r] + atomicAdd(&fill[r], 1);
     pairs[pos] = short(i);  // i = s * n + k
   }
-  for (int i = tid; i < kBetaSamples * n; i += blockDim.x) rowsum[i] = 0.0;
-  __syncthreads();
-  // ---- K_mixed row sums: D rows of the union, chunk by chunk, in LDS
+  // ---- K_mixed row sums, chunk by chunk
   const int R = C.rows;
-  const int g = tid >> 4, gl = tid & 15, ng = blockDim.x >> 4;
+  const int half = tid >> 9, jt = tid & 511;  // two threads per column, alternate rows
+  const int Ms = (M + 1) & ~1;
+  float fj[kFr];
+  if (jt < M) load_row(Fr, jt, fj);
+  __syncthreads();
+  MPCMMD_STAMP(p, 17);
+  const int g = tid >> 4, gl = tid & 15, ng = kKerThreads >> 4;
   for (int c0 = 0; c0 < U; c0 += R) {
     const int rc = min(R, U - c0);
-    for (int idx = tid; idx < rc * M; idx += blockDim.x) {
-      const int u = idx / M, j = idx - u * M;
-      const int r = ulist[c0 + u];
-      float d = fabsf(Fl[r] - Fl[j]);
-      for (int f = 1; f < kF; ++f) d = d + fabsf(Fl[f * M + r] - Fl[f * M + j]);
-      Dl[idx] = d;
+    for (int u = half; u < rc; u += 2) {
+      float fr[kFr];
+      load_row(Fr, ulist[c0 + u], fr);  // wave-uniform address: LDS broadcast
+      const float d = l1_22(fr, fj);
+      if (jt < M) Dl[u * Ms + jt] = d;
+      if (jt == M && (M & 1)) Dl[u * Ms + jt] = __builtin_inff();  // pad: exp2(-inf) = 0
     }
     __syncthreads();
+    if (c0 == 0) MPCMMD_STAMP(p, 18);
     const int p0 = start[ulist[c0]];
     const int p1 = start[ulist[c0 + rc - 1]] + cnt[ulist[c0 + rc - 1]];
     for (int pi = p0 + g; pi < p1; pi += ng) {
       const int i = pairs[pi];
       const int s = i / n;
-      const int u = urank[sl[i]] - c0;
-      const float sgm = sg[s], rs = rsg[s];
-      const float* drow = Dl + size_t(u) * M;
-      float acc = 0.0f;
-      for (int j = gl; j < M; j += 16) acc += __expf(div_rc(-drow[j], sgm, rs));
-      double a = double(acc);
+      const float cn = csg[s];
+      const f2* drow = reinterpret_cast<const f2*>(Dl + size_t(urank[sl[i]] - c0) * Ms);
+      const f2 c2 = {cn, cn};
+      f2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f};
+      const int J = Ms >> 1;
+      int j = gl;
+      for (; j + 16 < J; j += 32) {
+        const f2 t0 = drow[j] * c2, t1 = drow[j + 16] * c2;
+        a0 += f2{__builtin_amdgcn_exp2f(t0.x), __builtin_amdgcn_exp2f(t0.y)};
+        a1 += f2{__builtin_amdgcn_exp2f(t1.x), __builtin_amdgcn_exp2f(t1.y)};
+      }
+      if (j < J) {
+        const f2 t0 = drow[j] * c2;
+        a0 += f2{__builtin_amdgcn_exp2f(t0.x), __builtin_amdgcn_exp2f(t0.y)};
+      }
+      a0 += a1;
+      double a = double(a0.x) + double(a0.y);
       a += __shfl_xor(a, 1, 16);
       a += __shfl_xor(a, 2, 16);
       a += __shfl_xor(a, 4, 16);
@@ -395,94 +597,123 @@ __global__ __launch_bounds__(kThreads) void k_bkernel(Params p, int tb) {
       if (gl == 0) rowsum[i] = a;
     }
     __syncthreads();
+    if (c0 == 0) MPCMMD_STAMP(p, 19);
   }
-  // ---- K_red, QP (compute_beta_reduced) and cost, one wave per sample
-  const size_t qpw = (size_t(n) * (n + 1) / 2) * 8 + 32 * 33 * 4 + 32 * 8 + 64;
-  char* qbase = smem + C.work + size_t(w) * qpw;
-  double* Lp = reinterpret_cast<double*>(qbase);                                      // packed lower
-  float* Kl = reinterpret_cast<float*>(qbase + (size_t(n) * (n + 1) / 2) * 8);         // [32][33]
-  double* bl = reinterpret_cast<double*>(qbase + (size_t(n) * (n + 1) / 2) * 8 + 32 * 33 * 4);
+  MPCMMD_STAMP(p, 20);
+  // ---- QP per sample: 2 samples per wave (half-waves), lane = row
+  const int hw = lane >> 5, li = lane & 31;
+  const int tri = n * (n + 1) / 2, ntask = n * (n - 1) / 2;
+  double* Lp = reinterpret_cast<double*>(smem + C.work) + size_t(w * 2 + hw) * ker_qp_slot(n);
+  double* rinv = Lp + tri;
   const double inv_m = double(1.0f / float(M));
-  for (int s = w; s < kBetaSamples; s += nw) {
-    const float sgm = sg[s], rs = rsg[s];
-    const int ti = lane < n ? sl[s * n + lane] : 0;
-    if (lane < n) {
-      const int rowoff = lane * (lane + 1) / 2;
-      for (int k = 0; k < n; ++k) {
-        const int tk = sl[s * n + k];
-        float d = fabsf(Fl[ti] - Fl[tk]);
-        for (int f = 1; f < kF; ++f) d = d + fabsf(Fl[f * M + ti] - Fl[f * M + tk]);
-        const float kv = __expf(div_rc(-d, sgm, rs));
-        Kl[lane * 33 + k] = kv;
-        if (k <= lane) Lp[rowoff + k] = double(k == lane ? kv + 0.05f : kv);
-      }
+  const double delta = double(1.0f + 0.05f) - 1.0;  // C_ii - K_ii (K_ii = exp(0) = 1)
+  for (int s0 = 2 * w; s0 < kBetaSamples; s0 += 2 * nw) {
+    const int s = s0 + hw;
+    const bool sok = s < kBetaSamples;
+    const float cn = sok ? csg[s] : 0.0f;
+    const short* ss = sl + (sok ? s : 0) * n;
+    // strict lower triangle of K_red, tasks spread over the half-wave
+    for (int e = li; e < ntask; e += 32) {
+      int i = int((1.0f + sqrtf(1.0f + 8.0f * float(e))) * 0.5f);
+      while (i * (i - 1) / 2 > e) --i;
+      while ((i + 1) * i / 2 <= e) ++i;
+      const int k = e - i * (i - 1) / 2;
+      float fa[kFr], fb[kFr];
+      load_row(Fr, ss[i], fa);
+      load_row(Fr, ss[k], fb);
+      const float kv = __builtin_amdgcn_exp2f(l1_22(fa, fb) * cn);
+      if (sok) Lp[i * (i + 1) / 2 + k] = double(kv);
     }
+    if (li < n && sok) Lp[li * (li + 1) / 2 + li] = double(1.0f + 0.05f);
     wave_sync();
-    // left-looking Cholesky, lane = row
+    if (s0 == 0) MPCMMD_STAMP(p, 22);
+    // left-looking Cholesky, lane = row (rows live in the packed LDS triangle)
+    const bool act = sok && li < n;
+    const int ro = li * (li + 1) / 2;
     for (int j = 0; j < n; ++j) {
+      const int rj = j * (j + 1) / 2;
       double sv = 0.0;
-      if (lane >= j && lane < n) {
-        const int ri = lane * (lane + 1) / 2, rj = j * (j + 1) / 2;
-        sv = Lp[ri + j];
-        for (int k = 0; k < j; ++k) sv -= Lp[ri + k] * Lp[rj + k];
-        if (lane == j) Lp[ri + j] = sqrt(sv);
+      if (act && li >= j) {
+        double q0 = 0.0, q1 = 0.0, q2 = 0.0, q3 = 0.0;
+        int k = 0;
+        for (; k + 3 < j; k += 4) {
+          q0 = fma(Lp[ro + k], Lp[rj + k], q0);
+          q1 = fma(Lp[ro + k + 1], Lp[rj + k + 1], q1);
+          q2 = fma(Lp[ro + k + 2], Lp[rj + k + 2], q2);
+          q3 = fma(Lp[ro + k + 3], Lp[rj + k + 3], q3);
+        }
+        for (; k < j; ++k) q0 = fma(Lp[ro + k], Lp[rj + k], q0);
+        sv = Lp[ro + j] - ((q0 + q1) + (q2 + q3));
+        if (li == j) {
+          sv = sqrt(sv);
+          Lp[ro + j] = sv;
+          rinv[j] = 1.0 / sv;
+        }
       }
       wave_sync();
-      if (lane > j && lane < n) Lp[lane * (lane + 1) / 2 + j] = sv / Lp[j * (j + 1) / 2 + j];
+      if (act && li > j) Lp[ro + j] = sv * rinv[j];
       wave_sync();
     }
-    // two right-hand sides: g = rowsum / M (= -lincost) and 1 (the constraint column)
-    double a1 = lane < n ? rowsum[s * n + lane] * inv_m : 0.0, a2 = lane < n ? 1.0 : 0.0;
-    for (int j = 0; j < n; ++j) {  // forward, column-oriented
-      double y1 = 0.0, y2 = 0.0;
-      if (lane == j) {
-        const double dj = Lp[j * (j + 1) / 2 + j];
-        y1 = a1 / dj;
-        y2 = a2 / dj;
-        a1 = y1;
-        a2 = y2;
+    if (s0 == 0) MPCMMD_STAMP(p, 23);
+    // forward: L y = (g, 1)
+    const double gi = act ? rowsum[s * n + li] * inv_m : 0.0;
+    double a1 = gi, a2 = act ? 1.0 : 0.0;
+    for (int j = 0; j < n; ++j) {
+      if (act && li == j) {
+        const double r = rinv[j];
+        a1 = a1 * r;
+        a2 = a2 * r;
       }
-      y1 = __shfl(y1, j, 64);
-      y2 = __shfl(y2, j, 64);
-      if (lane > j && lane < n) {
-        const double lij = Lp[lane * (lane + 1) / 2 + j];
-        a1 -= lij * y1;
-        a2 -= lij * y2;
+      const double y1 = bcast_half(a1, j, hw), y2 = bcast_half(a2, j, hw);
+      if (act && li > j) {
+        const double l = Lp[ro + j];
+        a1 -= l * y1;
+        a2 -= l * y2;
       }
     }
-    for (int j = n - 1; j >= 0; --j) {  // backward with L^T
-      double x1 = 0.0, x2 = 0.0;
-      if (lane == j) {
-        const double dj = Lp[j * (j + 1) / 2 + j];
-        x1 = a1 / dj;
-        x2 = a2 / dj;
-        a1 = x1;
-        a2 = x2;
+    if (s0 == 0) MPCMMD_STAMP(p, 24);
+    // backward: L^T x = y
+    for (int j = n - 1; j >= 0; --j) {
+      if (li == j) {
+        const double r = rinv[j];
+        a1 = a1 * r;
+        a2 = a2 * r;
       }
-      x1 = __shfl(x1, j, 64);
-      x2 = __shfl(x2, j, 64);
-      if (lane < j) {
-        const double lji = Lp[j * (j + 1) / 2 + lane];
+      const double x1 = bcast_half(a1, j, hw), x2 = bcast_half(a2, j, hw);
+      if (act && li < j) {
+        const double lji = Lp[j * (j + 1) / 2 + li];
         a1 -= lji * x1;
         a2 -= lji * x2;
       }
     }
-    // beta = x1 + ((1 - sum x1) / sum x2) x2   (KKT with 1^T beta = 1)
-    const double s1 = wave_sum(lane < n ? a1 : 0.0), s2 = wave_sum(lane < n ? a2 : 0.0);
-    const float beta = lane < n ? float(a1 + ((1.0 - s1) / s2) * a2) : 0.0f;
-    if (lane < n) bl[lane] = double(beta);
-    wave_sync();
-    double kb = 0.0, qb = 0.0;
-    if (lane < n) {
-      for (int k = 0; k < n; ++k) kb += double(Kl[lane * 33 + k]) * bl[k];
-      kb *= double(beta);
-      qb = (-2.0 * (rowsum[s * n + lane] * inv_m)) * double(beta);
+    if (s0 == 0) MPCMMD_STAMP(p, 25);
+    double s1 = act ? a1 : 0.0, s2 = act ? a2 : 0.0;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      s1 += __shfl_xor(s1, o, 32);
+      s2 += __shfl_xor(s2, o, 32);
     }
-    const double cost = wave_sum(kb) + wave_sum(qb);
-    if (lane < n) p.btop[(size_t(b) * kBetaSamples + s) * n + lane] = beta;
-    if (lane == 0) p.bcost[size_t(b) * kBetaSamples + s] = float(cost);
+    const float beta = act ? float(a1 + ((1.0 - s1) / s2) * a2) : 0.0f;
+    // cost = |L^T beta|^2 - delta |beta|^2 - 2 g^T beta
+    const double bd = double(beta);
+    double lt = 0.0;
+    for (int k = 0; k < n; ++k) {
+      const double bk = bcast_half(bd, k, hw);
+      if (act && k >= li) lt += Lp[k * (k + 1) / 2 + li] * bk;
+    }
+    double c1 = act ? lt * lt : 0.0, c2 = act ? bd * bd : 0.0, c3 = act ? gi * bd : 0.0;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      c1 += __shfl_xor(c1, o, 32);
+      c2 += __shfl_xor(c2, o, 32);
+      c3 += __shfl_xor(c3, o, 32);
+    }
+    if (act) p.btop[(size_t(b) * kBetaSamples + s) * n + li] = beta;
+    if (sok && li == 0) p.bcost[size_t(b) * kBetaSamples + s] = float((c1 - delta * c2) - 2.0 * c3);
     wave_sync();
   }
+  __syncthreads();
+  MPCMMD_STAMP(p, 21);
 }
 
 // ------------------------------------------------------------------------
@@ -494,11 +725,8 @@ struct EliteLds {
 HDI EliteLds elite_lds(int M1) {
   EliteLds L{};
   const int nblk = (M1 + 15) / 16;
-  size_t u = size_t(M1) * 11 * 8;
-  const size_t pbuf = size_t(8) * 11 * 64 * 8;  // generate() scratch aliases U
-  if (u < pbuf) u = pbuf;
   L.U = 0;
-  L.Gb = (u + 15) & ~size_t(15);
+  L.Gb = (size_t(M1) * 11 * 8 + 15) & ~size_t(15);
   L.misc = L.Gb + ((size_t(nblk) * 66 * 8 + 15) & ~size_t(15));
   L.total = L.misc + 1024;
   return L;
@@ -539,26 +767,26 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
   __syncthreads();
   const int imin = info[1] ? info[0] : elite[0];  // jnp.argmin: first NaN, else first minimum
   if (tid == 0) p.res_beta[size_t(b) * kBetaIters + tb] = info[1] ? __int_as_float(0x7fc00000) : cst[elite[0]];
-  // ---- E_new = the 11 elite sample vectors (rows 0..10 of the next samples)
+  // ---- E_new = the 11 elite sample vectors (rows 0..10 of the next samples):
+  // previous elites, this iteration's new samples (ygen), or at tb = 0 the
+  // initial samples
   const float* Eold = p.belite + (size_t(tb & 1) * p.B + b) * kBetaElite * M1;
   float* Enew = p.belite + (size_t((tb + 1) & 1) * p.B + b) * kBetaElite * M1;
+  const int ys = ygen_stride(M);
+  const float* Y = p.ygen + size_t(b) * kNew * ys;
   for (int i = tid; i < kBetaElite * M1; i += blockDim.x) {
     const int q = i / M1, j = i - q * M1;
     const int e = elite[q];
+    float v;
     if (tb == 0) {
-      float v = float(kSqrt20 * double(p.beta_z0[size_t(e) * M1 + j]));
+      v = float(kSqrt20 * double(p.beta_z0[size_t(e) * M1 + j]));
       if (j == M) v = fmaxf(v, 0.01f);
-      Enew[i] = v;
     } else if (e < kBetaElite) {
-      Enew[i] = Eold[size_t(e) * M1 + j];
+      v = Eold[size_t(e) * M1 + j];
+    } else {
+      v = Y[size_t(e - kBetaElite) * ys + j];
     }
-  }
-  if (tb > 0) {  // elites that were new samples: regenerate them (generators of tb-1)
-    generate(
-        p, b, tb - 1,
-        [&](int l) { return (l < kBetaElite && elite[l] >= kBetaElite) ? elite[l] - kBetaElite : -1; },
-        [&](int l, int j, float y) { Enew[size_t(l) * M1 + j] = j == M ? fmaxf(y, 0.01f) : y; },
-        reinterpret_cast<double*>(smem + C.U));
+    Enew[i] = v;
   }
   __syncthreads();
   // ---- outputs of the beta-CEM on its last iteration (compute_beta.py:152-157)
@@ -602,7 +830,7 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
     for (int blk = 0; blk < nblk; ++blk) {
       const double g = Gb[blk * 66 + tid];
       Gb[blk * 66 + tid] = acc;
-      acc += g / kRidge;
+      acc = fma(g, kInvRidge, acc);
     }
   }
   __syncthreads();
@@ -617,24 +845,28 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
 #pragma unroll
       for (int a = 0; a < 11; ++a) uk[a] = Ul[k * 11 + a];
 #pragma unroll
-      for (int a = 0; a < 11; ++a)
+      for (int a = 0; a < 11; ++a) {
+        const double ua = uk[a] * kInvRidge;
 #pragma unroll
-        for (int c = a; c < 11; ++c) A[sym11(a, c)] += uk[a] * uk[c] / kRidge;
+        for (int c = a; c < 11; ++c) A[sym11(a, c)] = fma(ua, uk[c], A[sym11(a, c)]);
+      }
     }
-    // Cholesky A = R^T R (R upper, stored in A)
+    // Cholesky A = R^T R (R upper, stored in A; rinv = 1 / diag)
+    double rinv[11];
 #pragma unroll
     for (int a = 0; a < 11; ++a) {
       double d = A[sym11(a, a)];
 #pragma unroll
-      for (int k = 0; k < a; ++k) d -= A[sym11(k, a)] * A[sym11(k, a)];
+      for (int k = 0; k < a; ++k) d = fma(-A[sym11(k, a)], A[sym11(k, a)], d);
       d = sqrt(d);
       A[sym11(a, a)] = d;
+      rinv[a] = 1.0 / d;
 #pragma unroll
       for (int c = a + 1; c < 11; ++c) {
         double s = A[sym11(a, c)];
 #pragma unroll
-        for (int k = 0; k < a; ++k) s -= A[sym11(k, a)] * A[sym11(k, c)];
-        A[sym11(a, c)] = s / d;
+        for (int k = 0; k < a; ++k) s = fma(-A[sym11(k, a)], A[sym11(k, c)], s);
+        A[sym11(a, c)] = s * rinv[a];
       }
     }
     double u[11], v[11];
@@ -645,25 +877,26 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
     for (int a = 0; a < 11; ++a) {
       double s = u[a];
 #pragma unroll
-      for (int k = 0; k < a; ++k) s -= A[sym11(k, a)] * v[k];
-      v[a] = s / A[sym11(a, a)];
+      for (int k = 0; k < a; ++k) s = fma(-A[sym11(k, a)], v[k], s);
+      v[a] = s * rinv[a];
     }
     // R v = y
 #pragma unroll
     for (int a = 10; a >= 0; --a) {
       double s = v[a];
 #pragma unroll
-      for (int k = a + 1; k < 11; ++k) s -= A[sym11(a, k)] * v[k];
-      v[a] = s / A[sym11(a, a)];
+      for (int k = a + 1; k < 11; ++k) s = fma(-A[sym11(a, k)], v[k], s);
+      v[a] = s * rinv[a];
     }
     double uv = 0.0;
 #pragma unroll
-    for (int a = 0; a < 11; ++a) uv += u[a] * v[a];
+    for (int a = 0; a < 11; ++a) uv = fma(u[a], v[a], uv);
     const double ljj = sqrt(kRidge + uv);
+    const double rl = 1.0 / ljj;
     double* g = gen + size_t(j) * kGenStride;
 #pragma unroll
     for (int a = 0; a < 11; ++a) {
-      g[a] = v[a] / ljj;
+      g[a] = v[a] * rl;
       g[11 + a] = u[a];
     }
     g[22] = ljj;
@@ -761,7 +994,7 @@ __global__ __launch_bounds__(64) void k_mmdfinal(Params p, int t) {
   }
 }
 
-int samples_per_round(int M1) { return size_t(M1) * 65 * 4 <= 140 * 1024 ? 64 : 32; }
+
 
 }  // namespace
 
@@ -777,6 +1010,10 @@ bool mmdopt_supported(int n, int H, int O, std::string* why) {
     return false;
   }
   const EliteLds e = elite_lds(M + 1);
+  if (bs_lds(M + 1) > kLdsBudget) {
+    if (why) *why = "mmd_opt: num_reduced^2 too large for the sampling stage";
+    return false;
+  }
   if (e.total > kLdsBudget) {
     if (why) *why = "mmd_opt: num_reduced^2 too large for the elite stage";
     return false;
@@ -791,17 +1028,12 @@ void launch_mother(const Params& p, int t, hipStream_t s) {
 }
 
 void launch_bsample(const Params& p, int tb, hipStream_t s) {
-  const int M1 = p.M + 1, spr = samples_per_round(M1);
-  size_t ybytes = size_t(M1) * (spr + 1) * 4;
-  const size_t pbytes = size_t(8) * 11 * 64 * 8;
-  if (ybytes < pbytes) ybytes = pbytes;
-  const size_t lds = ((ybytes + 15) & ~size_t(15)) + size_t(8) * 64 * 4;
-  hipLaunchKernelGGL(k_bsample, dim3(p.B), dim3(kThreads), lds, s, p, tb, spr);
+  hipLaunchKernelGGL(k_bsample, dim3(p.B), dim3(kThreads), bs_lds(p.M + 1), s, p, tb);
 }
 
 void launch_bkernel(const Params& p, int tb, hipStream_t s) {
   const KerLds k = ker_lds(p.M, p.n, kLdsBudget);
-  hipLaunchKernelGGL(k_bkernel, dim3(p.B), dim3(kThreads), k.total, s, p, tb);
+  hipLaunchKernelGGL(k_bkernel, dim3(p.B), dim3(kKerThreads), k.total, s, p, tb);
 }
 
 void launch_belite(const Params& p, int tb, hipStream_t s) {

@@ -6,6 +6,8 @@
 
 #include <string>
 
+#define HDI_CONST __host__ __device__ __forceinline__ constexpr
+
 namespace mpcmmd {
 
 constexpr int kMaxH = 100;
@@ -17,6 +19,7 @@ constexpr int kEliteCost = 20;         // cem.py:140
 constexpr int kElite = 5;              // cem.py:138
 constexpr int kResultStride = 11 + 11 + 2 + 1 + 20 + kMaxReduced;  // cx, cy, lane, obs, sigma, res_beta, beta
 constexpr int kGenStride = 24;         // doubles per position in Params::gen
+HDI_CONST int ygen_stride(int M) { return ((M + 1) + 31) & ~31; }
 
 struct Params {
   // shapes / configuration
@@ -71,6 +74,9 @@ struct Params {
   double* gen;             // [B][M+1][kGenStride] W (11), U (11), L_jj
   float* genm;             // [B][M+1]     float32 elite mean
   int32_t* bestsel;        // [B][n]       reduced set of the best sample
+  float* ygen;             // [B][89][ygs] new samples of the current beta-iteration (ygs = M+1 rounded to 32)
+  // phase timestamps (s_memrealtime, 100 MHz) of workgroup 0, for profiling
+  unsigned long long* dbg;  // [64]
   // outputs
   float* results;          // [T][kResultStride]
   int32_t* tr_proj;        // [T][B]

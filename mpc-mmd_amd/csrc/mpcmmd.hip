@@ -359,6 +359,7 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
       p.gen = (double*)h->alloc("gen", size_t(B) * M1 * kGenStride * 8);
       p.genm = (float*)h->alloc("genm", size_t(B) * M1 * 4);
       p.bestsel = (int32_t*)h->alloc("bestsel", size_t(B) * n * 4);
+      p.ygen = (float*)h->alloc("ygen", size_t(B) * (kBetaSamples - kBetaElite) * ygen_stride(h->M) * 4);
     }
     p.pop = (float*)h->alloc("pop", size_t(2) * B * 8 * 4);
     p.mean = (float*)h->alloc("mean", 8 * 4);
@@ -377,6 +378,7 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
     p.beta = (float*)h->alloc("beta", size_t(B) * h->n * 4);
     p.sigma = (float*)h->alloc("sigma", size_t(B) * 4);
     p.res_beta = (float*)h->alloc("res_beta", size_t(B) * kBetaIters * 4);
+    p.dbg = (unsigned long long*)h->alloc("dbg", 64 * 8);
     p.results = (float*)h->alloc("results", size_t(T) * kResultStride * 4);
     p.tr_proj = (int32_t*)h->alloc("tr_proj", size_t(T) * B * 4);
     p.tr_obs = (int32_t*)h->alloc("tr_obs", size_t(T) * kEliteCost * 4);
