@@ -49,35 +49,42 @@ WORKLOADS = {
                  num_batch=1024),
 }
 
-FP32_PEAK_TFLOPS = 157.3   # MI355X fp32 vector (= fp32 MFMA) peak, MI355X_MICROARCH.md
+# MI355X peaks (MI355X_MICROARCH.md): fp32 vector 157.3 TFLOP/s = 78.6 T lane-ops/s
+# (one fp32 op per lane per cycle at full packing); HBM3E 8 TB/s
+VALU_PEAK_TOPS = 78.6
 HBM_PEAK_GBS = 8000.0
 
 
-def kernel_work(w, name):
-    """Algorithmic work of ONE launch of kernel `name` (Kernels).
-    Returns (kind, amount): kind "flop" (fp32/fp64 VALU ops, exp = 1) or
-    "byte" (HBM bytes)."""
+def kernel_work(w, name, launches, stats):
+    """Algorithmic work of the profiled launches of kernel `name`, in fp32
+    lane-operations (DESIGN.md, Kernels):
+      bkernel   per candidate and beta-iteration: U distinct mother rows x M
+                columns x 22 features x 2 (sub, abs-add), U measured by the
+                kernel (stats[0]); 100 x n (sample, row) pairs x M terms x 3
+                (scale, exp, add); n(n-1)/2 K_red entries per sample x 3
+      risk_baseline  B x S rollouts x H steps x (bicycle step 40 + 9 per obstacle)
+    Returns (kind, ops) or None when no model is defined."""
     B, H, O = w["num_batch"], w["num_prime"], w["num_obs"]
     n = w["num_reduced"]
     M = n * n
     if name == "bkernel":
-        # per candidate and beta-iteration: every distinct mother row's L1
-        # distances to all M rows (22 features, sub + abs-add = 2 flop) with
-        # the distinct-row count bounded by M, and for each of the 100 x n
-        # (sample, reduced row) pairs M Laplace terms (div 3, exp 2, add 1)
-        return "flop", B * (M * M * 22 * 2 + 100 * n * M * 6)
+        return "ops", stats[0] * M * 22 * 2 + launches * B * 100 * (n * M * 3 + n * (n - 1) // 2 * 3)
     if name == "risk_baseline":
-        S = n
-        per_rollout_step = 40 + O * 9          # bicycle step (4 transcendentals) + f_bar per obstacle
         beta = 2 * 160 if w["noise"] == "beta" else 0
-        return "flop", B * S * H * (per_rollout_step + beta)
-    if name == "mother":
-        return "flop", B * M * H * (40 + 44)    # bicycle step + fp64 fit accumulation (22 FMA)
-    if name == "bsample":
-        return "flop", B * (89 * (M + 1) * 2 * 11 * 2 + 100 * M * 4)
-    if name == "belite":
-        return "flop", B * ((M + 1) * (11 * 11 * 3 + 11 * 11 * 2 + 60))
-    return "flop", 0
+        return "ops", launches * B * n * H * (40 + O * 9 + beta)
+    return None
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC pass
+    (profiles/r01_pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE per the
+    MI355X guide's gfx950 correction), or None."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(kernel)
+    except (OSError, ValueError):
+        return None
 
 
 def make_workload(w, rank):
@@ -206,11 +213,13 @@ def main():
         dist.barrier()
     res = h.finish()
     # profiled pass (same steps, HIP events around every launch on the library's stream)
+    h.write("stats", np.zeros(8, np.uint64))
     h.profile(True)
     run(0, a.profile_steps)
     h.sync()
     kt = h.kernel_times()
     h.profile(False)
+    stats = h.read("stats", np.uint64).astype(np.int64)
     # final gather of per-config results over RCCL (§8e)
     vec = np.concatenate([res["cx"], res["cy"], [res["cost_lane"], res["cost_obs"]]]).astype(np.float32)
     if world > 1:
@@ -227,13 +236,12 @@ def main():
         dom = max(busy, key=lambda k: busy[k][1])
         launches, tot_ms = busy[dom]
         avg_s = tot_ms / launches / 1e3
-        kind, amount = kernel_work(w, dom)
-        if kind == "byte":
-            roof = {"bound": "hbm", "achieved": amount / avg_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
-        else:
-            roof = {"bound": "valu", "achieved": amount / avg_s / 1e12, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s"}
-        roof["frac"] = roof["achieved"] / roof["peak"]
-        roof["traffic"] = None
+        model = kernel_work(w, dom, launches, stats)
+        roof = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_TOPS, "unit": "Tops/s", "frac": None}
+        if model is not None:
+            roof["achieved"] = model[1] / launches / avg_s / 1e12
+            roof["frac"] = roof["achieved"] / VALU_PEAK_TOPS
+        roof["traffic"] = pmc_traffic(dom)
         roof["kernel"] = dom
         roof["avg_us"] = avg_s * 1e6
         line = {

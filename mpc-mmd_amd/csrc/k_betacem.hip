@@ -5,17 +5,19 @@
 //   k_mother    noisy control rows, n^2 mother rollouts (Cartesian product,
 //               cem_helper.py:469-530) with the ridge fit folded into the scan
 //               (compute_coeff, cem_helper.py:553-564) -> 22 features per row
-//   20 x { k_bsample  samples of the beta-CEM and their top-n |beta| rows
-//                     (compute_beta.py:41-49, 51-68, 117-118)
-//          k_bkernel  Laplace-kernel row sums over the mother set, K_red, the
-//                     equality-constrained QP and its cost per sample
-//                     (kernel_computation.py:19-65, compute_beta.py:70-91, 120-129)
+//   20 x { k_bsample  new samples of the beta-CEM (compute_beta.py:51-68)
+//          k_bselect  top-n |beta| rows and sigma per sample (compute_beta.py:41-49, 117-118)
+//          k_bkernel  Laplace-kernel row sums over the mother set and K_red
+//                     (kernel_computation.py:19-65, compute_beta.py:120-127)
+//          k_bqp      the equality-constrained QP and its cost per sample
+//                     (compute_beta.py:70-91, 129)
 //          k_belite   elite 11, mean, structured Cholesky of
 //                     cov = D D^T / 10 + 0.05 I, next generators (compute_beta.py:51-68, 133-145) }
 //   k_mmdfinal  reduced-set rollouts, collision residual, MMD obs / lane
 //               (costs.py:121-135, 173-186)
 //
-// All kernels: one 512-thread workgroup per candidate (the candidate's beta-CEM
+// k_bselect and k_bqp are latency-bound chains and run as many single-wave
+// workgroups; the others use one workgroup per candidate (the candidate's beta-CEM
 // is sequential over its 20 iterations; candidates are independent).
 //
 // The covariance of the beta-CEM is rank <= 10 plus 0.05 I
@@ -110,7 +112,8 @@ DEVI void load_keys(V val, int M, uint32_t* key) {
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     const int j = lane + 64 * q;
-    key[q] = j < M ? sort_key(fabsf(val(j))) : 0u;  // real keys have bit 31 set
+    const float v = val(min(j, M - 1));
+    key[q] = j < M ? sort_key(fabsf(v)) : 0u;  // real keys have bit 31 set
   }
 }
 
@@ -201,15 +204,10 @@ DEVI void select_batch(Row row, Out out, int first, int last, int stride, int M,
   constexpr int NB = NQ <= 8 ? 4 : (NQ <= 12 ? 2 : 1);
   for (int s0 = first; s0 < last; s0 += NB * stride) {
     uint32_t key[NB][NQ];
-    int nb = 0;
+    const int nb = min(NB, (last - s0 + stride - 1) / stride);
 #pragma unroll
-    for (int u = 0; u < NB; ++u) {
-      const int s = s0 + u * stride;
-      if (s < last) {
-        load_keys<NQ>(row(s), M, key[u]);
-        nb = u + 1;
-      }
-    }
+    for (int u = 0; u < NB; ++u)  // unconditional (clamped) loads: one memory latency
+      load_keys<NQ>(row(min(s0 + u * stride, last - 1)), M, key[u]);
     uint32_t T[NB];
     bool exact[NB];
     find_thresholds<NQ, NB>(key, nb, n, T, exact);
@@ -247,7 +245,7 @@ DEVI void select_rows(Row row, Out out, int first, int last, int stride, int M, 
 }
 
 // ------------------------------------------------------------------------
-// k_bsample: the 100 samples of beta-CEM iteration tb and their top-n rows.
+// k_bsample: the new samples of beta-CEM iteration tb >= 1.
 //
 // New samples (rows 11..99) use the structured Cholesky (file header):
 // lanes = samples, waves = position blocks, two passes (block partial sums
@@ -259,46 +257,22 @@ DEVI void select_rows(Row row, Out out, int first, int last, int stride, int M, 
 constexpr int kZChunk = 16;  // positions per register chunk of normals in the generation
 HDI size_t bs_gbytes(int M1) { return (size_t(M1) * kGenStride * 8 + 15) & ~size_t(15); }
 HDI size_t bs_pbytes() { return size_t(8) * 11 * 64 * 8; }
-HDI size_t bs_lds(int M1) { return bs_gbytes(M1) + bs_pbytes() + size_t(8) * 64 * 4; }
+HDI size_t bs_lds(int M1) { return bs_gbytes(M1) + bs_pbytes(); }
 
 __global__ __launch_bounds__(kThreads) void k_bsample(Params p, int tb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int b = blockIdx.x, M = p.M, M1 = M + 1, n = p.n;
+  const int b = blockIdx.x, M = p.M, M1 = M + 1;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6, lane = threadIdx.x & 63;
   double* Gl = reinterpret_cast<double*>(smem);
   double* Pbuf = reinterpret_cast<double*>(smem + bs_gbytes(M1));
-  int* wscr = reinterpret_cast<int*>(smem + bs_gbytes(M1) + bs_pbytes()) + w * 64;
-  int32_t* sel = p.bsel + size_t(b) * kBetaSamples * n;
-  float* sig = p.bsig + size_t(b) * kBetaSamples;
   MPCMMD_STAMP(p, 0);
-  if (tb == 0) {
-    // initial samples MVN(0, 20 I) with chol(20 I) = sqrt(20) I (compute_beta.py:41-49)
-    select_rows(
-        [&](int s) {
-          const float* z0 = p.beta_z0 + size_t(s) * M1;
-          return [=](int j) { return float(kSqrt20 * double(z0[j])); };
-        },
-        [&](int s) { return sel + s * n; }, w, kBetaSamples, nw, M, n, wscr);
-    if (threadIdx.x < kBetaSamples)
-      sig[threadIdx.x] = fmaxf(float(kSqrt20 * double(p.beta_z0[size_t(threadIdx.x) * M1 + M])), 0.01f);
-    return;
-  }
   // generators of iteration tb-1 -> LDS (W 0..10, U 11..21, L_jj 22, m 23)
   const double* G = p.gen + size_t(b) * M1 * kGenStride;
   const float* gm = p.genm + size_t(b) * M1;
-  for (int i = threadIdx.x; i < M1 * kGenStride; i += blockDim.x) {
-    const int j = i / kGenStride, k = i - j * kGenStride;
-    Gl[i] = k == 23 ? double(gm[j]) : G[i];
-  }
-  // rows 0..10: the previous iteration's elites (compute_beta.py:62)
-  const float* E = p.belite + (size_t(tb & 1) * p.B + b) * kBetaElite * M1;
-  select_rows(
-      [&](int s) {
-        const float* e = E + size_t(s) * M1;
-        return [=](int j) { return e[j]; };
-      },
-      [&](int s) { return sel + s * n; }, w, kBetaElite, nw, M, n, wscr);
-  if (threadIdx.x < kBetaElite) sig[threadIdx.x] = E[size_t(threadIdx.x) * M1 + M];
+#pragma unroll 4
+  for (int i = threadIdx.x; i < M1 * kGenStride; i += blockDim.x) Gl[i] = G[i];
+  __syncthreads();
+  for (int j = threadIdx.x; j < M1; j += blockDim.x) Gl[j * kGenStride + 23] = double(gm[j]);
   __syncthreads();
   MPCMMD_STAMP(p, 1);
   // rows 11..99: mean + L z (compute_beta.py:63), 64 samples per round
@@ -316,8 +290,8 @@ __global__ __launch_bounds__(kThreads) void k_bsample(Params p, int tb) {
     auto load = [&](float* zc, int c0) {
 #pragma unroll
       for (int q = 0; q < kZChunk; ++q) {
-        const int j = c0 + q;
-        zc[q] = j < j1 ? z[size_t(j) * kNew + sz] : 0.0f;
+        const int j = min(c0 + q, M);
+        zc[q] = z[size_t(j) * kNew + sz];
       }
     };
     double P[11];
@@ -375,19 +349,39 @@ __global__ __launch_bounds__(kThreads) void k_bsample(Params p, int tb) {
       load(za, c0 + 2 * kZChunk);
       passB(zb, c0 + kZChunk);
     }
-    __syncthreads();
-    MPCMMD_STAMP(p, 2 + 2 * (r0 >> 6));
-    select_rows(
-        [&](int sl) {
-          const float* y = Y + size_t(r0 + sl) * ys;
-          return [=](int j) { return y[j]; };
-        },
-        [&](int sl) { return sel + (kBetaElite + r0 + sl) * n; }, w, ns, nw, M, n, wscr);
-    if (threadIdx.x < ns) sig[kBetaElite + r0 + threadIdx.x] = Y[size_t(r0 + threadIdx.x) * ys + M];
-    MPCMMD_STAMP(p, 3 + 2 * (r0 >> 6));
+    __syncthreads();  // Pbuf reuse in the next round
+    MPCMMD_STAMP(p, 2 + (r0 >> 6));
   }
-  __syncthreads();
-  MPCMMD_STAMP(p, 15);
+}
+
+// ------------------------------------------------------------------------
+// k_bselect: top-n |beta| rows (compute_beta.py:117-118) and sigma of the
+// 100 samples.  Latency-bound per wave (ballot chains), so it runs as many
+// single-wave workgroups: wave (b, g) handles samples g, g+25, g+50, g+75.
+constexpr int kSelGroups = 25;
+
+__global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
+  __shared__ int scratch[64];
+  const int b = blockIdx.x, g = blockIdx.y, M = p.M, M1 = M + 1, n = p.n;
+  int32_t* sel = p.bsel + size_t(b) * kBetaSamples * n;
+  float* sig = p.bsig + size_t(b) * kBetaSamples;
+  const float* E = p.belite + (size_t(tb & 1) * p.B + b) * kBetaElite * M1;
+  const int ys = ygen_stride(M);
+  const float* Y = p.ygen + size_t(b) * kNew * ys;
+  const float* z0 = p.beta_z0;
+  // sample s: initial MVN(0, 20 I) draws (tb = 0, compute_beta.py:41-49), the
+  // previous elites (rows 0..10) or this iteration's new samples
+  auto row = [&](int s) {
+    const float* r = tb == 0 ? z0 + size_t(s) * M1 : (s < kBetaElite ? E + size_t(s) * M1 : Y + size_t(s - kBetaElite) * ys);
+    const bool scale = tb == 0;
+    return [=](int j) { return scale ? float(kSqrt20 * double(r[j])) : r[j]; };
+  };
+  select_rows(row, [&](int s) { return sel + s * n; }, g, kBetaSamples, kSelGroups, M, n, scratch);
+  if (threadIdx.x < 4) {
+    const int s = g + threadIdx.x * kSelGroups;
+    const float v = row(s)(M);
+    sig[s] = tb == 0 ? fmaxf(v, 0.01f) : v;  // later rows are clipped when written
+  }
 }
 
 // ------------------------------------------------------------------------
@@ -410,13 +404,10 @@ constexpr int kKerThreads = 1024;
 constexpr int kFr = 24;  // row-major feature stride (floats): 22 + pad for b128 reads
 
 struct KerLds {
-  size_t Fr, sel, csg, rowsum, cnt, start, fill, ulist, urank, pairs, work, total;
+  size_t Fr, sel, csg, rowsum, cnt, start, fill, ulist, urank, pairs, pair_s, work, total;
   int rows;  // D-chunk rows
 };
 
-// per half-wave: packed lower triangle (n(n+1)/2 doubles) + 1/L_jj (32 doubles)
-HDI size_t ker_qp_slot(int n) { return size_t(n) * (n + 1) / 2 + 32; }
-HDI size_t ker_qp_bytes(int n) { return size_t(kKerThreads / 64) * 2 * ker_qp_slot(n) * 8; }
 
 HDI KerLds ker_lds(int M, int n, size_t budget) {
   KerLds L{};
@@ -436,16 +427,14 @@ HDI KerLds ker_lds(int M, int n, size_t budget) {
   L.ulist = take(size_t(M) * 4);
   L.urank = take(size_t(M) * 4);
   L.pairs = take(size_t(kBetaSamples) * n * 2);
+  L.pair_s = take(size_t(kBetaSamples) * n);
   L.work = o;
   const size_t rest = budget > o ? budget - o : 0;
   const int Ms = (M + 1) & ~1;  // even row stride: float2 reads
   int rows = int(rest / (size_t(Ms) * 4));
   if (rows > 128) rows = 128;
   L.rows = rows;
-  size_t work = size_t(rows) * Ms * 4;
-  const size_t qp = ker_qp_bytes(n);
-  if (work < qp) work = qp;
-  L.total = o + work;
+  L.total = o + size_t(rows) * Ms * 4;
   return L;
 }
 
@@ -487,7 +476,7 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x, M = p.M, n = p.n;
   const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6), nw = kKerThreads >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const KerLds C = ker_lds(M, n, kLdsBudget);
   float* Fr = reinterpret_cast<float*>(smem + C.Fr);
   short* sl = reinterpret_cast<short*>(smem + C.sel);
@@ -499,13 +488,17 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb) {
   int* ulist = reinterpret_cast<int*>(smem + C.ulist);
   int* urank = reinterpret_cast<int*>(smem + C.urank);
   short* pairs = reinterpret_cast<short*>(smem + C.pairs);
+  unsigned char* pair_s = reinterpret_cast<unsigned char*>(smem + C.pair_s);
   float* Dl = reinterpret_cast<float*>(smem + C.work);
   const float* Fg = p.feat + size_t(b) * kF * M;
   MPCMMD_STAMP(p, 16);
-  for (int i = tid; i < kFr * M; i += kKerThreads) {
-    const int j = i / kFr, f = i - j * kFr;
-    Fr[i] = f < kF ? Fg[size_t(f) * M + j] : 0.0f;
+  // features [22][M] (global) -> rows [M][24] (LDS)
+#pragma unroll 4
+  for (int i = tid; i < kF * M; i += kKerThreads) {
+    const int f = i / M, j = i - f * M;
+    Fr[j * kFr + f] = Fg[i];
   }
+  for (int j = tid; j < M; j += kKerThreads) Fr[j * kFr + 22] = Fr[j * kFr + 23] = 0.0f;
   const int32_t* gsel = p.bsel + size_t(b) * kBetaSamples * n;
   for (int i = tid; i < kBetaSamples * n; i += kKerThreads) sl[i] = short(gsel[i]);
   for (int s = tid; s < kBetaSamples; s += kKerThreads) csg[s] = kNegLog2e / p.bsig[size_t(b) * kBetaSamples + s];
@@ -543,10 +536,12 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb) {
   }
   __syncthreads();
   const int U = urank[M - 1] + (cnt[M - 1] > 0);
+  if (tid == 0) atomicAdd(&p.stats[0], static_cast<unsigned long long>(U));
   for (int i = tid; i < kBetaSamples * n; i += kKerThreads) {
     const int r = sl[i];
     const int pos = start[r] + atomicAdd(&fill[r], 1);
     pairs[pos] = short(i);  // i = s * n + k
+    pair_s[pos] = static_cast<unsigned char>(i / n);
   }
   // ---- K_mixed row sums, chunk by chunk
   const int R = C.rows;
@@ -556,7 +551,8 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb) {
   if (jt < M) load_row(Fr, jt, fj);
   __syncthreads();
   MPCMMD_STAMP(p, 17);
-  const int g = tid >> 4, gl = tid & 15, ng = kKerThreads >> 4;
+  const int g = tid >> 3, gl = tid & 7, ng = kKerThreads >> 3;  // 8 lanes per pair
+  const int ntri = n * (n - 1) / 2;
   for (int c0 = 0; c0 < U; c0 += R) {
     const int rc = min(R, U - c0);
     for (int u = half; u < rc; u += 2) {
@@ -570,17 +566,19 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb) {
     if (c0 == 0) MPCMMD_STAMP(p, 18);
     const int p0 = start[ulist[c0]];
     const int p1 = start[ulist[c0 + rc - 1]] + cnt[ulist[c0 + rc - 1]];
+    const int J = Ms >> 1;
     for (int pi = p0 + g; pi < p1; pi += ng) {
       const int i = pairs[pi];
-      const int s = i / n;
+      const int s = pair_s[pi];
+      const int k = i - s * n;
       const float cn = csg[s];
-      const f2* drow = reinterpret_cast<const f2*>(Dl + size_t(urank[sl[i]] - c0) * Ms);
+      const int u = urank[sl[i]] - c0;
+      const f2* drow = reinterpret_cast<const f2*>(Dl + size_t(u) * Ms);
       const f2 c2 = {cn, cn};
       f2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f};
-      const int J = Ms >> 1;
       int j = gl;
-      for (; j + 16 < J; j += 32) {
-        const f2 t0 = drow[j] * c2, t1 = drow[j + 16] * c2;
+      for (; j + 8 < J; j += 16) {
+        const f2 t0 = drow[j] * c2, t1 = drow[j + 8] * c2;
         a0 += f2{__builtin_amdgcn_exp2f(t0.x), __builtin_amdgcn_exp2f(t0.y)};
         a1 += f2{__builtin_amdgcn_exp2f(t1.x), __builtin_amdgcn_exp2f(t1.y)};
       }
@@ -589,131 +587,159 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb) {
         a0 += f2{__builtin_amdgcn_exp2f(t0.x), __builtin_amdgcn_exp2f(t0.y)};
       }
       a0 += a1;
-      double a = double(a0.x) + double(a0.y);
-      a += __shfl_xor(a, 1, 16);
-      a += __shfl_xor(a, 2, 16);
-      a += __shfl_xor(a, 4, 16);
-      a += __shfl_xor(a, 8, 16);
-      if (gl == 0) rowsum[i] = a;
+      // K_red[s][k][kk] for kk < k: row t_k of the distance matrix is in the chunk
+      const float* dr = Dl + size_t(u) * Ms;
+      float* kr = p.bkred + (size_t(b) * kBetaSamples + s) * ntri + k * (k - 1) / 2;
+      for (int kk = gl; kk < k; kk += 8) kr[kk] = __builtin_amdgcn_exp2f(dr[sl[s * n + kk]] * cn);
+      float a = a0.x + a0.y;
+      a += __shfl_xor(a, 1, 8);
+      a += __shfl_xor(a, 2, 8);
+      a += __shfl_xor(a, 4, 8);
+      if (gl == 0) rowsum[i] = double(a);
     }
     __syncthreads();
     if (c0 == 0) MPCMMD_STAMP(p, 19);
   }
+  for (int i = tid; i < kBetaSamples * n; i += kKerThreads) p.brow[size_t(b) * kBetaSamples * n + i] = rowsum[i];
   MPCMMD_STAMP(p, 20);
-  // ---- QP per sample: 2 samples per wave (half-waves), lane = row
+}
+
+// ------------------------------------------------------------------------
+// k_bqp: compute_beta_reduced (compute_beta.py:70-91) for every sample, 2
+// samples per single-wave workgroup (half-waves, lane = row): left-looking
+// fp64 Cholesky of C = K_red + 0.05 I with the lane's row in registers (NP =
+// n rounded up to 8; padding rows are identity, their right-hand sides 0),
+// two triangular solves (g and 1), beta = x1 + ((1 - sum x1)/sum x2) x2,
+// cost = beta^T K beta - 2 g^T beta with beta^T C beta = |L^T beta|^2.
+// Latency-bound chains, hence many small workgroups.
+template <int NP>
+DEVI void bqp_solve(const Params& p, double* Lp, double* rinv) {
+  const int b = blockIdx.x, M = p.M, n = p.n, lane = threadIdx.x;
   const int hw = lane >> 5, li = lane & 31;
-  const int tri = n * (n + 1) / 2, ntask = n * (n - 1) / 2;
-  double* Lp = reinterpret_cast<double*>(smem + C.work) + size_t(w * 2 + hw) * ker_qp_slot(n);
-  double* rinv = Lp + tri;
+  const int s = blockIdx.y * 2 + hw;
+  const int ntri = n * (n - 1) / 2;
   const double inv_m = double(1.0f / float(M));
   const double delta = double(1.0f + 0.05f) - 1.0;  // C_ii - K_ii (K_ii = exp(0) = 1)
-  for (int s0 = 2 * w; s0 < kBetaSamples; s0 += 2 * nw) {
-    const int s = s0 + hw;
-    const bool sok = s < kBetaSamples;
-    const float cn = sok ? csg[s] : 0.0f;
-    const short* ss = sl + (sok ? s : 0) * n;
-    // strict lower triangle of K_red, tasks spread over the half-wave
-    for (int e = li; e < ntask; e += 32) {
-      int i = int((1.0f + sqrtf(1.0f + 8.0f * float(e))) * 0.5f);
-      while (i * (i - 1) / 2 > e) --i;
-      while ((i + 1) * i / 2 <= e) ++i;
-      const int k = e - i * (i - 1) / 2;
-      float fa[kFr], fb[kFr];
-      load_row(Fr, ss[i], fa);
-      load_row(Fr, ss[k], fb);
-      const float kv = __builtin_amdgcn_exp2f(l1_22(fa, fb) * cn);
-      if (sok) Lp[i * (i + 1) / 2 + k] = double(kv);
+  const bool sok = s < kBetaSamples;
+  const int sc = sok ? s : 0;
+  const bool act = sok && li < n;
+  const bool row_ok = li < NP;
+  const float* kr = p.bkred + (size_t(b) * kBetaSamples + sc) * ntri;
+  // own row of C in registers
+  double r[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    double v = 0.0;
+    if (k < li && li < n) v = double(kr[li * (li - 1) / 2 + k]);
+    if (k == li) v = li < n ? double(1.0f + 0.05f) : 1.0;
+    r[k] = v;
+  }
+  const double gi = act ? p.brow[(size_t(b) * kBetaSamples + s) * n + li] * inv_m : 0.0;
+  double* myrow = Lp + li * NP;
+  // left-looking Cholesky: row j of L is read from LDS (broadcast)
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const double* rj = Lp + j * NP;
+    double q0 = 0.0, q1 = 0.0;
+#pragma unroll
+    for (int k = 0; k + 1 < j; k += 2) {
+      q0 = fma(r[k], rj[k], q0);
+      q1 = fma(r[k + 1], rj[k + 1], q1);
     }
-    if (li < n && sok) Lp[li * (li + 1) / 2 + li] = double(1.0f + 0.05f);
+    if (j & 1) q0 = fma(r[j - 1], rj[j - 1], q0);
+    const double sv = r[j] - (q0 + q1);
+    if (li == j) {  // 1/sqrt by v_rsq_f64 + two Newton steps (no fp64 division)
+      double y = __builtin_amdgcn_rsq(sv);
+      y = y * fma(-0.5 * sv, y * y, 1.5);
+      y = y * fma(-0.5 * sv, y * y, 1.5);
+      const double d = sv * y;
+      r[j] = d;
+      rinv[j] = y;
+      myrow[j] = d;
+    }
     wave_sync();
-    if (s0 == 0) MPCMMD_STAMP(p, 22);
-    // left-looking Cholesky, lane = row (rows live in the packed LDS triangle)
-    const bool act = sok && li < n;
-    const int ro = li * (li + 1) / 2;
-    for (int j = 0; j < n; ++j) {
-      const int rj = j * (j + 1) / 2;
-      double sv = 0.0;
-      if (act && li >= j) {
-        double q0 = 0.0, q1 = 0.0, q2 = 0.0, q3 = 0.0;
-        int k = 0;
-        for (; k + 3 < j; k += 4) {
-          q0 = fma(Lp[ro + k], Lp[rj + k], q0);
-          q1 = fma(Lp[ro + k + 1], Lp[rj + k + 1], q1);
-          q2 = fma(Lp[ro + k + 2], Lp[rj + k + 2], q2);
-          q3 = fma(Lp[ro + k + 3], Lp[rj + k + 3], q3);
-        }
-        for (; k < j; ++k) q0 = fma(Lp[ro + k], Lp[rj + k], q0);
-        sv = Lp[ro + j] - ((q0 + q1) + (q2 + q3));
-        if (li == j) {
-          sv = sqrt(sv);
-          Lp[ro + j] = sv;
-          rinv[j] = 1.0 / sv;
-        }
-      }
-      wave_sync();
-      if (act && li > j) Lp[ro + j] = sv * rinv[j];
-      wave_sync();
+    if (row_ok && li > j) {
+      r[j] = sv * rinv[j];
+      myrow[j] = r[j];
     }
-    if (s0 == 0) MPCMMD_STAMP(p, 23);
-    // forward: L y = (g, 1)
-    const double gi = act ? rowsum[s * n + li] * inv_m : 0.0;
-    double a1 = gi, a2 = act ? 1.0 : 0.0;
-    for (int j = 0; j < n; ++j) {
-      if (act && li == j) {
-        const double r = rinv[j];
-        a1 = a1 * r;
-        a2 = a2 * r;
-      }
-      const double y1 = bcast_half(a1, j, hw), y2 = bcast_half(a2, j, hw);
-      if (act && li > j) {
-        const double l = Lp[ro + j];
-        a1 -= l * y1;
-        a2 -= l * y2;
-      }
-    }
-    if (s0 == 0) MPCMMD_STAMP(p, 24);
-    // backward: L^T x = y
-    for (int j = n - 1; j >= 0; --j) {
-      if (li == j) {
-        const double r = rinv[j];
-        a1 = a1 * r;
-        a2 = a2 * r;
-      }
-      const double x1 = bcast_half(a1, j, hw), x2 = bcast_half(a2, j, hw);
-      if (act && li < j) {
-        const double lji = Lp[j * (j + 1) / 2 + li];
-        a1 -= lji * x1;
-        a2 -= lji * x2;
-      }
-    }
-    if (s0 == 0) MPCMMD_STAMP(p, 25);
-    double s1 = act ? a1 : 0.0, s2 = act ? a2 : 0.0;
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-      s1 += __shfl_xor(s1, o, 32);
-      s2 += __shfl_xor(s2, o, 32);
-    }
-    const float beta = act ? float(a1 + ((1.0 - s1) / s2) * a2) : 0.0f;
-    // cost = |L^T beta|^2 - delta |beta|^2 - 2 g^T beta
-    const double bd = double(beta);
-    double lt = 0.0;
-    for (int k = 0; k < n; ++k) {
-      const double bk = bcast_half(bd, k, hw);
-      if (act && k >= li) lt += Lp[k * (k + 1) / 2 + li] * bk;
-    }
-    double c1 = act ? lt * lt : 0.0, c2 = act ? bd * bd : 0.0, c3 = act ? gi * bd : 0.0;
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-      c1 += __shfl_xor(c1, o, 32);
-      c2 += __shfl_xor(c2, o, 32);
-      c3 += __shfl_xor(c3, o, 32);
-    }
-    if (act) p.btop[(size_t(b) * kBetaSamples + s) * n + li] = beta;
-    if (sok && li == 0) p.bcost[size_t(b) * kBetaSamples + s] = float((c1 - delta * c2) - 2.0 * c3);
     wave_sync();
   }
-  __syncthreads();
-  MPCMMD_STAMP(p, 21);
+  // forward: L y = (g, 1); y_j handed to the half-wave through LDS
+  double2* xb = reinterpret_cast<double2*>(rinv + NP);
+  double a1 = gi, a2 = act ? 1.0 : 0.0;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    if (li == j) {
+      a1 = a1 * rinv[j];
+      a2 = a2 * rinv[j];
+      xb[j] = double2{a1, a2};
+    }
+    wave_sync();
+    if (li > j) {
+      const double2 y = xb[j];
+      a1 = fma(-r[j], y.x, a1);
+      a2 = fma(-r[j], y.y, a2);
+    }
+  }
+  // backward: L^T x = y (column li of L from LDS)
+#pragma unroll
+  for (int j = NP - 1; j >= 0; --j) {
+    if (li == j) {
+      a1 = a1 * rinv[j];
+      a2 = a2 * rinv[j];
+      xb[j] = double2{a1, a2};
+    }
+    wave_sync();
+    if (li < j) {
+      const double lji = Lp[j * NP + li];
+      const double2 x = xb[j];
+      a1 = fma(-lji, x.x, a1);
+      a2 = fma(-lji, x.y, a2);
+    }
+  }
+  double s1 = act ? a1 : 0.0, s2 = act ? a2 : 0.0;
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) {
+    s1 += __shfl_xor(s1, o, 32);
+    s2 += __shfl_xor(s2, o, 32);
+  }
+  const float beta = act ? float(a1 + ((1.0 - s1) / s2) * a2) : 0.0f;
+  // cost = |L^T beta|^2 - delta |beta|^2 - 2 g^T beta
+  const double bd = double(beta);
+  double* bl = reinterpret_cast<double*>(xb + NP);
+  if (li < NP) bl[li] = bd;
+  wave_sync();
+  double lt = 0.0;
+#pragma unroll
+  for (int k = 0; k < NP; ++k)
+    if (k >= li && li < NP) lt = fma(Lp[k * NP + li], bl[k], lt);
+  double c1 = act ? lt * lt : 0.0, c2 = act ? bd * bd : 0.0, c3 = act ? gi * bd : 0.0;
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) {
+    c1 += __shfl_xor(c1, o, 32);
+    c2 += __shfl_xor(c2, o, 32);
+    c3 += __shfl_xor(c3, o, 32);
+  }
+  if (act) p.btop[(size_t(b) * kBetaSamples + s) * n + li] = beta;
+  if (sok && li == 0) p.bcost[size_t(b) * kBetaSamples + s] = float((c1 - delta * c2) - 2.0 * c3);
+}
+
+HDI int qp_np(int n) { return (n + 7) & ~7; }
+// per half-wave: L rows (NP x NP doubles), 1/L_jj (NP), solve hand-off (2 NP), beta (NP)
+HDI size_t qp_slot(int np) { return size_t(np) * np + 4 * np; }
+HDI size_t ker_qp_bytes(int n) { return size_t(2) * qp_slot(qp_np(n)) * 8; }
+
+__global__ __launch_bounds__(64) void k_bqp(Params p, int tb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int np = qp_np(p.n), hw = threadIdx.x >> 5;
+  double* Lp = reinterpret_cast<double*>(smem) + size_t(hw) * qp_slot(np);
+  double* rinv = Lp + np * np;
+  switch (np) {
+    case 8: return bqp_solve<8>(p, Lp, rinv);
+    case 16: return bqp_solve<16>(p, Lp, rinv);
+    case 24: return bqp_solve<24>(p, Lp, rinv);
+    default: return bqp_solve<32>(p, Lp, rinv);
+  }
 }
 
 // ------------------------------------------------------------------------
@@ -1029,6 +1055,14 @@ void launch_mother(const Params& p, int t, hipStream_t s) {
 
 void launch_bsample(const Params& p, int tb, hipStream_t s) {
   hipLaunchKernelGGL(k_bsample, dim3(p.B), dim3(kThreads), bs_lds(p.M + 1), s, p, tb);
+}
+
+void launch_bselect(const Params& p, int tb, hipStream_t s) {
+  hipLaunchKernelGGL(k_bselect, dim3(p.B, kSelGroups), dim3(64), 0, s, p, tb);
+}
+
+void launch_bqp(const Params& p, int tb, hipStream_t s) {
+  hipLaunchKernelGGL(k_bqp, dim3(p.B, kBetaSamples / 2), dim3(64), ker_qp_bytes(p.n), s, p, tb);
 }
 
 void launch_bkernel(const Params& p, int tb, hipStream_t s) {

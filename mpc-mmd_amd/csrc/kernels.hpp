@@ -74,9 +74,14 @@ struct Params {
   double* gen;             // [B][M+1][kGenStride] W (11), U (11), L_jj
   float* genm;             // [B][M+1]     float32 elite mean
   int32_t* bestsel;        // [B][n]       reduced set of the best sample
+  double* brow;            // [B][100][n]  K_mixed row sums (fp64)
+  float* bkred;            // [B][100][n(n-1)/2] K_red strict lower triangle
   float* ygen;             // [B][89][ygs] new samples of the current beta-iteration (ygs = M+1 rounded to 32)
   // phase timestamps (s_memrealtime, 100 MHz) of workgroup 0, for profiling
   unsigned long long* dbg;  // [64]
+  // work counters for the roofline: [0] sum over k_bkernel workgroups of the
+  // distinct mother rows (distance rows computed)
+  unsigned long long* stats;  // [8]
   // outputs
   float* results;          // [T][kResultStride]
   int32_t* tr_proj;        // [T][B]
@@ -91,7 +96,9 @@ void launch_risk_baseline(const Params& p, int t, hipStream_t s);
 // mmd_opt risk, one launch each (mpcmmd.hip chains them)
 void launch_mother(const Params& p, int t, hipStream_t s);
 void launch_bsample(const Params& p, int tb, hipStream_t s);
+void launch_bselect(const Params& p, int tb, hipStream_t s);
 void launch_bkernel(const Params& p, int tb, hipStream_t s);
+void launch_bqp(const Params& p, int tb, hipStream_t s);
 void launch_belite(const Params& p, int tb, hipStream_t s);
 void launch_mmdfinal(const Params& p, int t, hipStream_t s);
 bool mmdopt_supported(int n, int H, int O, std::string* why);

@@ -46,14 +46,16 @@ enum KernelId {
   kKRiskBaseline,
   kKMother,
   kKBSample,
+  kKBSelect,
   kKBKernel,
+  kKBQp,
   kKBElite,
   kKMmdFinal,
   kKSelect,
   kNumKernels
 };
-const char* kKernelNames[kNumKernels] = {"noise",   "front",  "risk_baseline", "mother", "bsample",
-                                         "bkernel", "belite", "mmdfinal",      "select"};
+const char* kKernelNames[kNumKernels] = {"noise",   "front", "risk_baseline", "mother", "bsample", "bselect",
+                                         "bkernel", "bqp",   "belite",        "mmdfinal", "select"};
 
 }  // namespace
 
@@ -189,6 +191,16 @@ void gen_beta_tables(mpcmmd_handle* h) {
   h->beta_tables_internal = true;
 }
 
+// one beta-CEM iteration (compute_beta.py:112-147)
+void run_beta_iteration(mpcmmd_handle* h, int tb) {
+  const Params& p = h->p;
+  if (tb > 0) h->launch(kKBSample, [&] { launch_bsample(p, tb, h->stream); });
+  h->launch(kKBSelect, [&] { launch_bselect(p, tb, h->stream); });
+  h->launch(kKBKernel, [&] { launch_bkernel(p, tb, h->stream); });
+  h->launch(kKBQp, [&] { launch_bqp(p, tb, h->stream); });
+  h->launch(kKBElite, [&] { launch_belite(p, tb, h->stream); });
+}
+
 void run_stage(mpcmmd_handle* h, int stage, int t) {
   const Params& p = h->p;
   switch (stage) {
@@ -202,11 +214,7 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
       if (p.cost == MPCMMD_COST_MMD_OPT) {
         if (!h->mmd_ok) throw std::invalid_argument("mmd_opt unsupported for this configuration: " + h->mmd_why);
         h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
-        for (int tb = 0; tb < kBetaIters; ++tb) {
-          h->launch(kKBSample, [&] { launch_bsample(p, tb, h->stream); });
-          h->launch(kKBKernel, [&] { launch_bkernel(p, tb, h->stream); });
-          h->launch(kKBElite, [&] { launch_belite(p, tb, h->stream); });
-        }
+        for (int tb = 0; tb < kBetaIters; ++tb) run_beta_iteration(h, tb);
         h->launch(kKMmdFinal, [&] { launch_mmdfinal(p, t, h->stream); });
       } else
         h->launch(kKRiskBaseline, [&] { launch_risk_baseline(p, t, h->stream); });
@@ -222,8 +230,14 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
       if (p.cost != MPCMMD_COST_MMD_OPT || !h->mmd_ok) throw std::invalid_argument("stages 4-8 need cost mmd_opt");
       if (stage >= 5 && stage <= 7 && t >= kBetaIters) throw std::invalid_argument("beta-CEM iteration out of range");
       if (stage == 4) h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
-      if (stage == 5) h->launch(kKBSample, [&] { launch_bsample(p, t, h->stream); });
-      if (stage == 6) h->launch(kKBKernel, [&] { launch_bkernel(p, t, h->stream); });
+      if (stage == 5) {  // samples + their top-n rows
+        if (t > 0) h->launch(kKBSample, [&] { launch_bsample(p, t, h->stream); });
+        h->launch(kKBSelect, [&] { launch_bselect(p, t, h->stream); });
+      }
+      if (stage == 6) {  // kernel sums + QP
+        h->launch(kKBKernel, [&] { launch_bkernel(p, t, h->stream); });
+        h->launch(kKBQp, [&] { launch_bqp(p, t, h->stream); });
+      }
       if (stage == 7) h->launch(kKBElite, [&] { launch_belite(p, t, h->stream); });
       if (stage == 8) h->launch(kKMmdFinal, [&] { launch_mmdfinal(p, t, h->stream); });
       break;
@@ -359,6 +373,8 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
       p.gen = (double*)h->alloc("gen", size_t(B) * M1 * kGenStride * 8);
       p.genm = (float*)h->alloc("genm", size_t(B) * M1 * 4);
       p.bestsel = (int32_t*)h->alloc("bestsel", size_t(B) * n * 4);
+      p.brow = (double*)h->alloc("brow", size_t(B) * kBetaSamples * n * 8);
+      p.bkred = (float*)h->alloc("bkred", size_t(B) * kBetaSamples * (n * (n - 1) / 2) * 4);
       p.ygen = (float*)h->alloc("ygen", size_t(B) * (kBetaSamples - kBetaElite) * ygen_stride(h->M) * 4);
     }
     p.pop = (float*)h->alloc("pop", size_t(2) * B * 8 * 4);
@@ -379,6 +395,7 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
     p.sigma = (float*)h->alloc("sigma", size_t(B) * 4);
     p.res_beta = (float*)h->alloc("res_beta", size_t(B) * kBetaIters * 4);
     p.dbg = (unsigned long long*)h->alloc("dbg", 64 * 8);
+    p.stats = (unsigned long long*)h->alloc("stats", 8 * 8);
     p.results = (float*)h->alloc("results", size_t(T) * kResultStride * 4);
     p.tr_proj = (int32_t*)h->alloc("tr_proj", size_t(T) * B * 4);
     p.tr_obs = (int32_t*)h->alloc("tr_obs", size_t(T) * kEliteCost * 4);
