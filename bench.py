@@ -37,6 +37,7 @@ for _p in (ROOT, PKG):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
+kF = 22  # beta-CEM features per mother row (cx | cy)
 METRIC = "MPC optimizer steps/s (batch=1024,H=30,obs_samp=500) @1/2/4/8 GPU; % HBM roofline"
 
 # BASELINE.json configs[1] (headline) and configs[2]
@@ -58,17 +59,22 @@ HBM_PEAK_GBS = 8000.0
 def kernel_work(w, name, launches, stats):
     """Algorithmic work of the profiled launches of kernel `name`, in fp32
     lane-operations (DESIGN.md, Kernels):
-      bkernel   per candidate and beta-iteration: U distinct mother rows x M
-                columns x 22 features x 2 (sub, abs-add), U measured by the
-                kernel (stats[0]); 100 x n (sample, row) pairs x M terms x 3
-                (scale, exp, add); n(n-1)/2 K_red entries per sample x 3
+      bdist     per candidate and outer iteration: M x M distances x 22
+                features x 2 (sub, abs-add)
+      bkernel   per candidate and beta-iteration: the (sample, row) pairs
+                summed (counted by the kernel, stats[1]; 100 x n on the first
+                beta-iteration, 89 x n after) x (M exp terms + (n-1)/2 K_red
+                entries) x 3 (scale, exp, add)
       risk_baseline  B x S rollouts x H steps x (bicycle step 40 + 9 per obstacle)
     Returns (kind, ops) or None when no model is defined."""
     B, H, O = w["num_batch"], w["num_prime"], w["num_obs"]
     n = w["num_reduced"]
     M = n * n
     if name == "bkernel":
-        return "ops", stats[0] * M * 22 * 2 + launches * B * 100 * (n * M * 3 + n * (n - 1) // 2 * 3)
+        # pairs summed (stats[1]) x (M exp terms + (n-1)/2 K_red entries on average) x 3 (scale, exp, add)
+        return "ops", stats[1] * (M + (n - 1) / 2) * 3
+    if name == "bdist":
+        return "ops", launches * B * M * M * kF * 2
     if name == "risk_baseline":
         beta = 2 * 160 if w["noise"] == "beta" else 0
         return "ops", launches * B * n * H * (40 + O * 9 + beta)

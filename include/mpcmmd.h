@@ -173,8 +173,9 @@ int mpcmmd_write(mpcmmd_handle* h, const char* name, const void* src, size_t byt
  *   6 bkernel    kernel row sums, reduced QP, QP cost     (compute_beta.py:70-91, 120-129)
  *   7 belite     elites, mean, next generators             (compute_beta.py:51-68, 133-157)
  *   8 mmdfinal   reduced rollouts, MMD obs / lane          (costs.py:121-135, 173-186)
- * Buffer "beta_z" holds the device layout [20][M+1][89] (transposed on
- * upload in mpcmmd_begin; mpcmmd_write writes it raw). */
+ * Buffer "beta_z" holds the device layout [20][P][96], P = M+1 rounded up to
+ * 16, zero padded (transposed on upload in mpcmmd_begin; mpcmmd_write writes
+ * it raw). */
 int mpcmmd_run_stage(mpcmmd_handle* h, int32_t stage, int32_t t);
 
 /* Host-side batch-invariant constants (no GPU needed): fills dst with the

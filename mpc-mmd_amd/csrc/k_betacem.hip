@@ -42,6 +42,11 @@ constexpr double kSqrt20 = 4.47213595499957927704;   // chol(20 I) (compute_beta
 constexpr double kRidge = 0.05;                      // cov jitter (compute_beta.py:61)
 constexpr double kInvRidge = 20.0;
 
+// first sample a beta-iteration processes: from the second iteration on,
+// samples 0..10 are the previous iteration's elites, unchanged, and k_belite
+// carries their top-n rows, sigma, QP solution and cost
+HDI int first_sample(int tb) { return tb > 0 ? kBetaElite : 0; }
+
 #define kconst __attribute__((address_space(4)))
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -94,6 +99,46 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
     for (int k = 0; k < 11; ++k) {
       F[k * M + m] = float(cx[k]);
       F[(11 + k) * M + m] = float(cy[k]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------
+// k_bdist: the L1 distance matrix of the mother features,
+// D[a][b] = sum_f |F_a,f - F_b,f| (kernel_computation.py:33-39 with the
+// 22-dim features of compute_beta.py:120-124), once per outer iteration.
+// Every K_mixed / K_red entry the 20 beta-iterations need is exp(-D[a][b] /
+// sigma) for a selected row a, so the rows are computed once here instead
+// of 20 times.  Workgroup = (candidate, tile of kDistRows rows); a thread
+// owns one column (its 22 features in registers), the tile's row features
+// are LDS broadcasts; the feature sum is sequential (the oracle's order).
+// Pad columns M..Md-1 hold +inf so exp2(-inf) = 0 in the row sums.
+constexpr int kDistRows = 32;
+constexpr int kDistThreads = 256;
+
+__global__ __launch_bounds__(kDistThreads) void k_bdist(Params p) {
+  __shared__ __attribute__((aligned(16))) float Fr[kDistRows][kF + 2];
+  const int b = blockIdx.x, r0 = blockIdx.y * kDistRows, M = p.M, Md = dist_stride(M);
+  const int tid = threadIdx.x;
+  const float* Fg = p.feat + size_t(b) * kF * M;
+  for (int i = tid; i < kDistRows * kF; i += kDistThreads) {
+    const int r = i / kF, f = i - r * kF;
+    Fr[r][f] = r0 + r < M ? Fg[f * M + r0 + r] : 0.0f;
+  }
+  __syncthreads();
+  const int rn = min(kDistRows, M - r0);
+  float* D = p.bdist + (size_t(b) * M + r0) * Md;
+  for (int j = tid; j < Md; j += kDistThreads) {
+    float fj[kF];
+    const int jc = min(j, M - 1);
+#pragma unroll
+    for (int f = 0; f < kF; ++f) fj[f] = Fg[f * M + jc];
+    for (int r = 0; r < rn; ++r) {
+      const float* fr = Fr[r];  // wave-uniform: LDS broadcast
+      float d = fabsf(fr[0] - fj[0]);
+#pragma unroll
+      for (int f = 1; f < kF; ++f) d = d + fabsf(fr[f] - fj[f]);
+      D[size_t(r) * Md + j] = j < M ? d : __builtin_inff();
     }
   }
 }
@@ -245,113 +290,129 @@ DEVI void select_rows(Row row, Out out, int first, int last, int stride, int M, 
 }
 
 // ------------------------------------------------------------------------
-// k_bsample: the new samples of beta-CEM iteration tb >= 1.
+// k_bsample: the new samples of beta-CEM iteration tb >= 1 (rows 11..99,
+// mean + L z, compute_beta.py:51-68) with the structured factor of the file
+// header, as fp64 MFMA (v_mfma_f64_16x16x4_f64) over blocks of 16 positions:
 //
-// New samples (rows 11..99) use the structured Cholesky (file header):
-// lanes = samples, waves = position blocks, two passes (block partial sums
-// P = sum_j w_j z_j, then the scan y_j = m_j + L_jj z_j + u_j . S_j).  The
-// candidate's generators (W, U, L_jj, m per position, 192 B) are staged in
-// LDS once, so the serial chain over positions is LDS-broadcast bound.  The
-// samples go to ygen (global, row per sample) for the selection and for
-// k_belite's elite copy.
-constexpr int kZChunk = 16;  // positions per register chunk of normals in the generation
-HDI size_t bs_gbytes(int M1) { return (size_t(M1) * kGenStride * 8 + 15) & ~size_t(15); }
-HDI size_t bs_pbytes() { return size_t(8) * 11 * 64 * 8; }
-HDI size_t bs_lds(int M1) { return bs_gbytes(M1) + bs_pbytes(); }
+//   Y_c = m_c + T_c Z_c + U_c S_c,   S_{c+1} = S_c + W_c^T Z_c
+//
+// Z_c [16 positions x 16 samples] the normals, S_c [11 x 16] the prefix
+// sum_{j < 16c} w_j z_j, U_c / W_c [16 x 11] the generators u_j / w_j and
+// T_c [16 x 16] = strict_lower(U_c W_c^T) + diag(L_jj) (itself one MFMA
+// product, masked).  A wave owns kTilesPerWave tiles of 16 samples and walks
+// the blocks in order; S lives in accumulator registers and is, by the
+// 16x16x4 f64 layouts, directly the B operand of U_c S_c.  All in fp64 (the
+// oracle's dense fp64 Cholesky agrees to ~1e-15 before the fp32 rounding).
+//
+// f64 16x16x4 layouts (lane l, r = l & 15, h = l >> 4):
+//   A: A[r][h]   B: B[h][r]   C/D register i: C[h + 4 i][r]
+typedef double d4 __attribute__((ext_vector_type(4)));
+constexpr int kSampleTiles = kBzCols / 16;  // 6 tiles of 16 sample columns (89 used)
+constexpr int kTilesPerWave = 2;
+constexpr int kSampleWaves = kSampleTiles / kTilesPerWave;
+static_assert(kSampleTiles % kTilesPerWave == 0, "tiles per wave");
+static_assert(kBzCols >= kNew, "sample tiles");
 
-__global__ __launch_bounds__(kThreads) void k_bsample(Params p, int tb) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int b = blockIdx.x, M = p.M, M1 = M + 1;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6, lane = threadIdx.x & 63;
-  double* Gl = reinterpret_cast<double*>(smem);
-  double* Pbuf = reinterpret_cast<double*>(smem + bs_gbytes(M1));
-  MPCMMD_STAMP(p, 0);
-  // generators of iteration tb-1 -> LDS (W 0..10, U 11..21, L_jj 22, m 23)
-  const double* G = p.gen + size_t(b) * M1 * kGenStride;
-  const float* gm = p.genm + size_t(b) * M1;
-#pragma unroll 4
-  for (int i = threadIdx.x; i < M1 * kGenStride; i += blockDim.x) Gl[i] = G[i];
-  __syncthreads();
-  for (int j = threadIdx.x; j < M1; j += blockDim.x) Gl[j * kGenStride + 23] = double(gm[j]);
-  __syncthreads();
-  MPCMMD_STAMP(p, 1);
-  // rows 11..99: mean + L z (compute_beta.py:63), 64 samples per round
-  const float* z = p.beta_z + size_t(tb - 1) * M1 * kNew;  // device layout [M+1][89]
-  const int ys = ygen_stride(M);
-  float* Y = p.ygen + size_t(b) * kNew * ys;
-  const int bs = (M1 + nw - 1) / nw;
-  const int j0 = min(M1, w * bs), j1 = min(M1, j0 + bs);
-  for (int r0 = 0; r0 < kNew; r0 += 64) {
-    const int ns = min(64, kNew - r0);
-    const bool act = lane < ns;
-    const int sz = r0 + (act ? lane : 0);
-    // standard normals of this wave's positions, register double-buffered in
-    // chunks of 16 positions (the next chunk's loads fly during the FMAs)
-    auto load = [&](float* zc, int c0) {
+DEVI d4 mfma64(double a, double b, d4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
+
+// Operands of one block, loaded unconditionally (generators, means and
+// normals are zero padded to whole blocks and tiles; features >= 11 masked
+// by selects), so the loop has no branches and the compiler can count
+// outstanding loads exactly.
+struct SampleBlock {
+  double wA[4];  // W[p0 + 4k + h][r]        (A of W^T Z; r = feature)
+  double wX[3];  // W[p0 + r][4i + h]        (A of W U^T; 4i + h = feature)
+  double uX[3];  // U[p0 + r][4i + h]        (B of W U^T, A of U S)
+  double L;      // L_jj of position p0 + r
+  double m[4];   // mean of position p0 + h + 4i
+  double z[kTilesPerWave][4];  // Z[p0 + 4k + h][s0 + 16t + r]
+};
+
+DEVI void load_block(SampleBlock& q, const double* G, const float* gm, const float* z, int p0, int s0, int r,
+                     int h) {
 #pragma unroll
-      for (int q = 0; q < kZChunk; ++q) {
-        const int j = min(c0 + q, M);
-        zc[q] = z[size_t(j) * kNew + sz];
-      }
-    };
-    double P[11];
-#pragma unroll
-    for (int k = 0; k < 11; ++k) P[k] = 0.0;
-    auto passA = [&](const float* zc, int c0) {
-#pragma unroll
-      for (int q = 0; q < kZChunk; ++q) {
-        if (c0 + q >= j1) break;
-        const double zj = double(zc[q]);
-        const double* g = Gl + (c0 + q) * kGenStride;
-#pragma unroll
-        for (int k = 0; k < 11; ++k) P[k] = fma(g[k], zj, P[k]);
-      }
-    };
-    float za[kZChunk], zb[kZChunk];
-    load(za, j0);
-    for (int c0 = j0; c0 < j1; c0 += 2 * kZChunk) {
-      load(zb, c0 + kZChunk);
-      passA(za, c0);
-      load(za, c0 + 2 * kZChunk);
-      passA(zb, c0 + kZChunk);
-    }
-#pragma unroll
-    for (int k = 0; k < 11; ++k) Pbuf[(w * 11 + k) * 64 + lane] = P[k];
-    __syncthreads();
-    double S[11];
-#pragma unroll
-    for (int k = 0; k < 11; ++k) {
-      double c = 0.0;
-      for (int w2 = 0; w2 < w; ++w2) c = c + Pbuf[(w2 * 11 + k) * 64 + lane];
-      S[k] = c;
-    }
-    float* yrow = Y + size_t(sz) * ys;
-    auto passB = [&](const float* zc, int c0) {
-#pragma unroll
-      for (int q = 0; q < kZChunk; ++q) {
-        const int j = c0 + q;
-        if (j >= j1) break;
-        const double zj = double(zc[q]);
-        const double* g = Gl + j * kGenStride;
-        double d = 0.0;
-#pragma unroll
-        for (int k = 0; k < 11; ++k) d = fma(g[11 + k], S[k], d);
-        const double yv = fma(g[22], zj, g[23]) + d;
-#pragma unroll
-        for (int k = 0; k < 11; ++k) S[k] = fma(g[k], zj, S[k]);
-        if (act) yrow[j] = j == M ? fmaxf(float(yv), 0.01f) : float(yv);
-      }
-    };
-    load(za, j0);
-    for (int c0 = j0; c0 < j1; c0 += 2 * kZChunk) {
-      load(zb, c0 + kZChunk);
-      passB(za, c0);
-      load(za, c0 + 2 * kZChunk);
-      passB(zb, c0 + kZChunk);
-    }
-    __syncthreads();  // Pbuf reuse in the next round
-    MPCMMD_STAMP(p, 2 + (r0 >> 6));
+  for (int k = 0; k < 4; ++k) {
+    const double v = G[size_t(p0 + 4 * k + h) * kGenStride + r];
+    q.wA[k] = r < 11 ? v : 0.0;
   }
+  const double* g = G + size_t(p0 + r) * kGenStride;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int f = 4 * i + h;
+    const double vw = g[f], vu = g[11 + f];
+    q.wX[i] = f < 11 ? vw : 0.0;
+    q.uX[i] = f < 11 ? vu : 0.0;
+  }
+  q.L = g[22];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q.m[i] = double(gm[p0 + h + 4 * i]);
+#pragma unroll
+  for (int t = 0; t < kTilesPerWave; ++t)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q.z[t][k] = double(z[size_t(p0 + 4 * k + h) * kBzCols + s0 + 16 * t + r]);
+}
+
+__global__ __launch_bounds__(64 * kSampleWaves) void k_bsample(Params p, int tb) {
+  const int b = blockIdx.x, M = p.M, Pp = pos_pad(M);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, h = lane >> 4;
+  const int s0 = w * kTilesPerWave * 16;
+  MPCMMD_STAMP(p, 0);
+  const double* G = p.gen + size_t(b) * Pp * kGenStride;
+  const float* gm = p.genm + size_t(b) * Pp;
+  const float* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
+  const int ys = ygen_stride(M);
+  float* Y = p.ygen + (size_t(b) * kBzCols + s0 + r) * ys;
+  d4 S[kTilesPerWave];
+#pragma unroll
+  for (int t = 0; t < kTilesPerWave; ++t) S[t] = d4{0.0, 0.0, 0.0, 0.0};
+  const int nblk = Pp >> 4;
+  SampleBlock cur;
+  load_block(cur, G, gm, z, 0, s0, r, h);
+  for (int c = 0; c < nblk; ++c) {
+    const int p0 = c << 4;
+    SampleBlock nxt;
+    load_block(nxt, G, gm, z, min(p0 + 16, Pp - 16), s0, r, h);  // prefetch (last block: reload)
+    // X = W_c U_c^T: register i holds w_{h+4i} . u_r = T[row r][col h + 4i]
+    d4 X = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) X = mfma64(cur.wX[i], cur.uX[i], X);
+    double T[4];  // A operand of T Z, k-step i: T[r][4i + h]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = h + 4 * i;
+      T[i] = k < r ? X[i] : (k == r ? cur.L : 0.0);
+    }
+    // independent chains, tiles interleaved: Y = m + T Z (acc a) + U S (acc b),
+    // P = W^T Z (two partial accumulators), S += P after U S has read S
+    d4 Ya[kTilesPerWave], Yb[kTilesPerWave], P0[kTilesPerWave], P1[kTilesPerWave];
+#pragma unroll
+    for (int t = 0; t < kTilesPerWave; ++t) {
+      Ya[t] = d4{cur.m[0], cur.m[1], cur.m[2], cur.m[3]};
+      Yb[t] = d4{0.0, 0.0, 0.0, 0.0};
+      P0[t] = d4{0.0, 0.0, 0.0, 0.0};
+      P1[t] = d4{0.0, 0.0, 0.0, 0.0};
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int t = 0; t < kTilesPerWave; ++t) {
+        if (k < 3) Yb[t] = mfma64(cur.uX[k], S[t][k], Yb[t]);
+        if (k & 1) P1[t] = mfma64(cur.wA[k], cur.z[t][k], P1[t]);
+        else P0[t] = mfma64(cur.wA[k], cur.z[t][k], P0[t]);
+        Ya[t] = mfma64(T[k], cur.z[t][k], Ya[t]);
+      }
+#pragma unroll
+    for (int t = 0; t < kTilesPerWave; ++t) {
+      S[t] = S[t] + (P0[t] + P1[t]);
+      const d4 Yv = Ya[t] + Yb[t];
+      float* yrow = Y + size_t(16 * t) * ys + p0 + h;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) yrow[4 * i] = p0 + h + 4 * i == M ? fmaxf(float(Yv[i]), 0.01f) : float(Yv[i]);
+    }
+    cur = nxt;
+  }
+  MPCMMD_STAMP(p, 1);
 }
 
 // ------------------------------------------------------------------------
@@ -367,7 +428,7 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
   float* sig = p.bsig + size_t(b) * kBetaSamples;
   const float* E = p.belite + (size_t(tb & 1) * p.B + b) * kBetaElite * M1;
   const int ys = ygen_stride(M);
-  const float* Y = p.ygen + size_t(b) * kNew * ys;
+  const float* Y = p.ygen + size_t(b) * kBzCols * ys;
   const float* z0 = p.beta_z0;
   // sample s: initial MVN(0, 20 I) draws (tb = 0, compute_beta.py:41-49), the
   // previous elites (rows 0..10) or this iteration's new samples
@@ -376,9 +437,12 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
     const bool scale = tb == 0;
     return [=](int j) { return scale ? float(kSqrt20 * double(r[j])) : r[j]; };
   };
-  select_rows(row, [&](int s) { return sel + s * n; }, g, kBetaSamples, kSelGroups, M, n, scratch);
-  if (threadIdx.x < 4) {
-    const int s = g + threadIdx.x * kSelGroups;
+  // samples 0..10 of iteration tb >= 1 are the previous elites, whose rows
+  // and sigma k_belite carried over
+  const int s_lo = first_sample(tb);
+  select_rows(row, [&](int s) { return sel + s * n; }, s_lo + g, kBetaSamples, kSelGroups, M, n, scratch);
+  const int s = s_lo + g + int(threadIdx.x) * kSelGroups;
+  if (threadIdx.x < 4 && s < kBetaSamples) {
     const float v = row(s)(M);
     sig[s] = tb == 0 ? fmaxf(v, 0.01f) : v;  // later rows are clipped when written
   }
@@ -387,27 +451,23 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
 // ------------------------------------------------------------------------
 // k_bkernel: one workgroup (1024 threads) per candidate.
 //
-//   rows     the distinct mother rows any sample selected (union, ~150 of 484
-//            on average; every K_mixed row is a row of the M x M mother
-//            distance matrix, kernel_computation.py:33-39)
-//   D chunk  rows of the L1 distance matrix in LDS, register-tiled: a thread
-//            owns one column j (its 22 features in registers) and walks the
-//            chunk's rows, whose features are LDS broadcasts
-//   pairs    (sample, reduced row) pairs sorted by row; a 16-lane group sums
-//            exp(-D[r][j] / sigma_s) over j (v_exp_f32 on d * (-log2 e / sigma))
-//   QP       2 samples per wave, lane = row: K_red (strict lower triangle
-//            spread over the half-wave), left-looking fp64 Cholesky of
-//            C = K_red + 0.05 I with the lane's row in registers, two
-//            triangular solves (g and 1), beta = x1 + ((1 - sum x1)/sum x2) x2,
-//            cost = beta^T K beta - 2 g^T beta with beta^T C beta = |L^T beta|^2
+//   rows     the distinct mother rows the samples selected (union, ~150 of
+//            484 on average); each is a row of the distance matrix k_bdist
+//            wrote this outer iteration (kernel_computation.py:33-39), staged
+//            into LDS chunk by chunk with 16-byte loads
+//   pairs    (sample, reduced row) pairs sorted by row; an 8-lane group sums
+//            exp(-D[r][j] / sigma_s) over j (v_exp_f32 on d * (-log2 e /
+//            sigma), packed scale / add), and writes the sample's K_red
+//            entries of that row
+// From the second beta-iteration on, samples 0..10 are the previous elites:
+// their selection, kernels and QP are unchanged, k_belite carried them, and
+// only samples 11..99 are processed here.
 constexpr int kKerThreads = 1024;
-constexpr int kFr = 24;  // row-major feature stride (floats): 22 + pad for b128 reads
 
 struct KerLds {
-  size_t Fr, sel, csg, rowsum, cnt, start, fill, ulist, urank, pairs, pair_s, work, total;
+  size_t sel, csg, rowsum, cnt, start, fill, ulist, urank, pairs, pair_s, work, total;
   int rows;  // D-chunk rows
 };
-
 
 HDI KerLds ker_lds(int M, int n, size_t budget) {
   KerLds L{};
@@ -417,7 +477,6 @@ HDI KerLds ker_lds(int M, int n, size_t budget) {
     o = (o + bytes + 15) & ~size_t(15);
     return at;
   };
-  L.Fr = take(size_t(M) * kFr * 4);
   L.sel = take(size_t(kBetaSamples) * n * 2);
   L.csg = take(size_t(kBetaSamples) * 4);
   L.rowsum = take(size_t(kBetaSamples) * n * 8);
@@ -430,55 +489,22 @@ HDI KerLds ker_lds(int M, int n, size_t budget) {
   L.pair_s = take(size_t(kBetaSamples) * n);
   L.work = o;
   const size_t rest = budget > o ? budget - o : 0;
-  const int Ms = (M + 1) & ~1;  // even row stride: float2 reads
-  int rows = int(rest / (size_t(Ms) * 4));
-  if (rows > 128) rows = 128;
+  int rows = int(rest / (size_t(dist_stride(M)) * 4));
+  if (rows > 256) rows = 256;
   L.rows = rows;
-  L.total = o + size_t(rows) * Ms * 4;
+  L.total = o + size_t(rows) * dist_stride(M) * 4;
   return L;
 }
 
 constexpr size_t kLdsBudget = 160 * 1024 - 1024;
 constexpr float kNegLog2e = -1.44269504088896340736f;
 
-// value of lane j of this half-wave (lanes 0..31 | 32..63), via readlane
-DEVI double bcast_half(double v, int j, int hw) {
-  const long long bits = __double_as_longlong(v);
-  const int lo = int(bits), hi = int(bits >> 32);
-  const int l0 = __builtin_amdgcn_readlane(lo, j), h0 = __builtin_amdgcn_readlane(hi, j);
-  const int l1 = __builtin_amdgcn_readlane(lo, j + 32), h1 = __builtin_amdgcn_readlane(hi, j + 32);
-  const long long r0 = (static_cast<long long>(h0) << 32) | static_cast<unsigned>(l0);
-  const long long r1 = (static_cast<long long>(h1) << 32) | static_cast<unsigned>(l1);
-  return __longlong_as_double(hw ? r1 : r0);
-}
-
-// sum_f |a_f - b_f| over the 22 features, sequential (oracle l1_dist order)
-DEVI float l1_22(const float* a, const float* b) {
-  float d = fabsf(a[0] - b[0]);
-#pragma unroll
-  for (int f = 1; f < kF; ++f) d = d + fabsf(a[f] - b[f]);
-  return d;
-}
-
-DEVI void load_row(const float* Fr, int r, float* out) {
-  const float4* s = reinterpret_cast<const float4*>(Fr + r * kFr);
-#pragma unroll
-  for (int q = 0; q < kFr / 4; ++q) {
-    const float4 v = s[q];
-    out[4 * q] = v.x;
-    out[4 * q + 1] = v.y;
-    out[4 * q + 2] = v.z;
-    out[4 * q + 3] = v.w;
-  }
-}
-
 __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int b = blockIdx.x, M = p.M, n = p.n;
+  const int b = blockIdx.x, M = p.M, n = p.n, Md = dist_stride(M);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const KerLds C = ker_lds(M, n, kLdsBudget);
-  float* Fr = reinterpret_cast<float*>(smem + C.Fr);
   short* sl = reinterpret_cast<short*>(smem + C.sel);
   float* csg = reinterpret_cast<float*>(smem + C.csg);
   double* rowsum = reinterpret_cast<double*>(smem + C.rowsum);
@@ -490,24 +516,19 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb) {
   short* pairs = reinterpret_cast<short*>(smem + C.pairs);
   unsigned char* pair_s = reinterpret_cast<unsigned char*>(smem + C.pair_s);
   float* Dl = reinterpret_cast<float*>(smem + C.work);
-  const float* Fg = p.feat + size_t(b) * kF * M;
+  const int s_lo = first_sample(tb);
+  const int i_lo = s_lo * n, i_hi = kBetaSamples * n;
   MPCMMD_STAMP(p, 16);
-  // features [22][M] (global) -> rows [M][24] (LDS)
-#pragma unroll 4
-  for (int i = tid; i < kF * M; i += kKerThreads) {
-    const int f = i / M, j = i - f * M;
-    Fr[j * kFr + f] = Fg[i];
-  }
-  for (int j = tid; j < M; j += kKerThreads) Fr[j * kFr + 22] = Fr[j * kFr + 23] = 0.0f;
   const int32_t* gsel = p.bsel + size_t(b) * kBetaSamples * n;
-  for (int i = tid; i < kBetaSamples * n; i += kKerThreads) sl[i] = short(gsel[i]);
-  for (int s = tid; s < kBetaSamples; s += kKerThreads) csg[s] = kNegLog2e / p.bsig[size_t(b) * kBetaSamples + s];
+  for (int i = i_lo + tid; i < i_hi; i += kKerThreads) sl[i] = short(gsel[i]);
+  for (int s = s_lo + tid; s < kBetaSamples; s += kKerThreads)
+    csg[s] = kNegLog2e / p.bsig[size_t(b) * kBetaSamples + s];
   for (int r = tid; r < M; r += kKerThreads) {
     cnt[r] = 0;
     fill[r] = 0;
   }
   __syncthreads();
-  for (int i = tid; i < kBetaSamples * n; i += kKerThreads) atomicAdd(&cnt[sl[i]], 1);
+  for (int i = i_lo + tid; i < i_hi; i += kKerThreads) atomicAdd(&cnt[sl[i]], 1);
   __syncthreads();
   if (w == 0) {  // exclusive scans of cnt and (cnt > 0), one wave
     const int per = (M + 63) / 64, a = lane * per, e = min(M, a + per);
@@ -536,44 +557,40 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb) {
   }
   __syncthreads();
   const int U = urank[M - 1] + (cnt[M - 1] > 0);
-  if (tid == 0) atomicAdd(&p.stats[0], static_cast<unsigned long long>(U));
-  for (int i = tid; i < kBetaSamples * n; i += kKerThreads) {
+  if (tid == 0) {
+    atomicAdd(&p.stats[0], static_cast<unsigned long long>(U));
+    atomicAdd(&p.stats[1], static_cast<unsigned long long>(i_hi - i_lo));
+  }
+  for (int i = i_lo + tid; i < i_hi; i += kKerThreads) {
     const int r = sl[i];
     const int pos = start[r] + atomicAdd(&fill[r], 1);
     pairs[pos] = short(i);  // i = s * n + k
     pair_s[pos] = static_cast<unsigned char>(i / n);
   }
-  // ---- K_mixed row sums, chunk by chunk
-  const int R = C.rows;
-  const int half = tid >> 9, jt = tid & 511;  // two threads per column, alternate rows
-  const int Ms = (M + 1) & ~1;
-  float fj[kFr];
-  if (jt < M) load_row(Fr, jt, fj);
-  __syncthreads();
   MPCMMD_STAMP(p, 17);
+  const float4* Dg = reinterpret_cast<const float4*>(p.bdist + size_t(b) * M * Md);
+  const int R = C.rows, q4 = Md >> 2;
   const int g = tid >> 3, gl = tid & 7, ng = kKerThreads >> 3;  // 8 lanes per pair
   const int ntri = n * (n - 1) / 2;
   for (int c0 = 0; c0 < U; c0 += R) {
     const int rc = min(R, U - c0);
-    for (int u = half; u < rc; u += 2) {
-      float fr[kFr];
-      load_row(Fr, ulist[c0 + u], fr);  // wave-uniform address: LDS broadcast
-      const float d = l1_22(fr, fj);
-      if (jt < M) Dl[u * Ms + jt] = d;
-      if (jt == M && (M & 1)) Dl[u * Ms + jt] = __builtin_inff();  // pad: exp2(-inf) = 0
+    __syncthreads();  // previous chunk consumed (and, first time, pairs built)
+    for (int idx = tid; idx < rc * q4; idx += kKerThreads) {
+      const int u = idx / q4, c = idx - u * q4;
+      reinterpret_cast<float4*>(Dl)[idx] = Dg[size_t(ulist[c0 + u]) * q4 + c];
     }
     __syncthreads();
     if (c0 == 0) MPCMMD_STAMP(p, 18);
     const int p0 = start[ulist[c0]];
     const int p1 = start[ulist[c0 + rc - 1]] + cnt[ulist[c0 + rc - 1]];
-    const int J = Ms >> 1;
+    const int J = Md >> 1;
     for (int pi = p0 + g; pi < p1; pi += ng) {
       const int i = pairs[pi];
       const int s = pair_s[pi];
       const int k = i - s * n;
       const float cn = csg[s];
       const int u = urank[sl[i]] - c0;
-      const f2* drow = reinterpret_cast<const f2*>(Dl + size_t(u) * Ms);
+      const f2* drow = reinterpret_cast<const f2*>(Dl + size_t(u) * Md);
       const f2 c2 = {cn, cn};
       f2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f};
       int j = gl;
@@ -588,7 +605,7 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb) {
       }
       a0 += a1;
       // K_red[s][k][kk] for kk < k: row t_k of the distance matrix is in the chunk
-      const float* dr = Dl + size_t(u) * Ms;
+      const float* dr = Dl + size_t(u) * Md;
       float* kr = p.bkred + (size_t(b) * kBetaSamples + s) * ntri + k * (k - 1) / 2;
       for (int kk = gl; kk < k; kk += 8) kr[kk] = __builtin_amdgcn_exp2f(dr[sl[s * n + kk]] * cn);
       float a = a0.x + a0.y;
@@ -597,156 +614,205 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb) {
       a += __shfl_xor(a, 4, 8);
       if (gl == 0) rowsum[i] = double(a);
     }
-    __syncthreads();
     if (c0 == 0) MPCMMD_STAMP(p, 19);
   }
-  for (int i = tid; i < kBetaSamples * n; i += kKerThreads) p.brow[size_t(b) * kBetaSamples * n + i] = rowsum[i];
+  __syncthreads();
+  for (int i = i_lo + tid; i < i_hi; i += kKerThreads) p.brow[size_t(b) * kBetaSamples * n + i] = rowsum[i];
   MPCMMD_STAMP(p, 20);
 }
 
 // ------------------------------------------------------------------------
-// k_bqp: compute_beta_reduced (compute_beta.py:70-91) for every sample, 2
-// samples per single-wave workgroup (half-waves, lane = row): left-looking
-// fp64 Cholesky of C = K_red + 0.05 I with the lane's row in registers (NP =
-// n rounded up to 8; padding rows are identity, their right-hand sides 0),
-// two triangular solves (g and 1), beta = x1 + ((1 - sum x1)/sum x2) x2,
-// cost = beta^T K beta - 2 g^T beta with beta^T C beta = |L^T beta|^2.
-// Latency-bound chains, hence many small workgroups.
-template <int NP>
-DEVI void bqp_solve(const Params& p, double* Lp, double* rinv) {
-  const int b = blockIdx.x, M = p.M, n = p.n, lane = threadIdx.x;
-  const int hw = lane >> 5, li = lane & 31;
-  const int s = blockIdx.y * 2 + hw;
-  const int ntri = n * (n - 1) / 2;
-  const double inv_m = double(1.0f / float(M));
-  const double delta = double(1.0f + 0.05f) - 1.0;  // C_ii - K_ii (K_ii = exp(0) = 1)
-  const bool sok = s < kBetaSamples;
-  const int sc = sok ? s : 0;
-  const bool act = sok && li < n;
-  const bool row_ok = li < NP;
-  const float* kr = p.bkred + (size_t(b) * kBetaSamples + sc) * ntri;
-  // own row of C in registers
-  double r[NP];
-#pragma unroll
-  for (int k = 0; k < NP; ++k) {
-    double v = 0.0;
-    if (k < li && li < n) v = double(kr[li * (li - 1) / 2 + k]);
-    if (k == li) v = li < n ? double(1.0f + 0.05f) : 1.0;
-    r[k] = v;
+// k_bqp: compute_beta_reduced (compute_beta.py:70-91) for every sample:
+// C = K_red + 0.05 I, C x1 = g, C x2 = 1, beta = x1 + ((1 - sum x1) / sum x2) x2
+// (the (n+1) KKT system), cost = beta^T K beta - 2 g^T beta with
+// beta^T C beta = |L^T beta|^2.  All in fp64.
+//
+// A quad (4 lanes) per QP, 16 QPs per wave: lane q owns rows i = 4t + q of
+// the (padded to NP) matrix, in registers.  Right-looking Cholesky; the
+// column entries every lane needs are quad broadcasts (DPP quad_perm, no
+// LDS, no barriers); the triangular solves are a row sweep (forward, quad
+// broadcast of y_j) and a column sweep (backward, quad sum of partials).
+// Entries above the diagonal are kept at exactly 0, padding rows are
+// identity with zero right-hand sides.
+template <int CTRL>
+DEVI double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, int(b), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+// value of quad lane l (0..3) in every lane of the quad; l is a constant
+// after unrolling, so the switch folds
+DEVI double quad_bcast(double v, int l) {
+  switch (l & 3) {
+    case 0: return dpp_d<0x00>(v);
+    case 1: return dpp_d<0x55>(v);
+    case 2: return dpp_d<0xAA>(v);
+    default: return dpp_d<0xFF>(v);
   }
-  const double gi = act ? p.brow[(size_t(b) * kBetaSamples + s) * n + li] * inv_m : 0.0;
-  double* myrow = Lp + li * NP;
-  // left-looking Cholesky: row j of L is read from LDS (broadcast)
-#pragma unroll
-  for (int j = 0; j < NP; ++j) {
-    const double* rj = Lp + j * NP;
-    double q0 = 0.0, q1 = 0.0;
-#pragma unroll
-    for (int k = 0; k + 1 < j; k += 2) {
-      q0 = fma(r[k], rj[k], q0);
-      q1 = fma(r[k + 1], rj[k + 1], q1);
-    }
-    if (j & 1) q0 = fma(r[j - 1], rj[j - 1], q0);
-    const double sv = r[j] - (q0 + q1);
-    if (li == j) {  // 1/sqrt by v_rsq_f64 + two Newton steps (no fp64 division)
-      double y = __builtin_amdgcn_rsq(sv);
-      y = y * fma(-0.5 * sv, y * y, 1.5);
-      y = y * fma(-0.5 * sv, y * y, 1.5);
-      const double d = sv * y;
-      r[j] = d;
-      rinv[j] = y;
-      myrow[j] = d;
-    }
-    wave_sync();
-    if (row_ok && li > j) {
-      r[j] = sv * rinv[j];
-      myrow[j] = r[j];
-    }
-    wave_sync();
-  }
-  // forward: L y = (g, 1); y_j handed to the half-wave through LDS
-  double2* xb = reinterpret_cast<double2*>(rinv + NP);
-  double a1 = gi, a2 = act ? 1.0 : 0.0;
-#pragma unroll
-  for (int j = 0; j < NP; ++j) {
-    if (li == j) {
-      a1 = a1 * rinv[j];
-      a2 = a2 * rinv[j];
-      xb[j] = double2{a1, a2};
-    }
-    wave_sync();
-    if (li > j) {
-      const double2 y = xb[j];
-      a1 = fma(-r[j], y.x, a1);
-      a2 = fma(-r[j], y.y, a2);
-    }
-  }
-  // backward: L^T x = y (column li of L from LDS)
-#pragma unroll
-  for (int j = NP - 1; j >= 0; --j) {
-    if (li == j) {
-      a1 = a1 * rinv[j];
-      a2 = a2 * rinv[j];
-      xb[j] = double2{a1, a2};
-    }
-    wave_sync();
-    if (li < j) {
-      const double lji = Lp[j * NP + li];
-      const double2 x = xb[j];
-      a1 = fma(-lji, x.x, a1);
-      a2 = fma(-lji, x.y, a2);
-    }
-  }
-  double s1 = act ? a1 : 0.0, s2 = act ? a2 : 0.0;
-#pragma unroll
-  for (int o = 1; o < 32; o <<= 1) {
-    s1 += __shfl_xor(s1, o, 32);
-    s2 += __shfl_xor(s2, o, 32);
-  }
-  const float beta = act ? float(a1 + ((1.0 - s1) / s2) * a2) : 0.0f;
-  // cost = |L^T beta|^2 - delta |beta|^2 - 2 g^T beta
-  const double bd = double(beta);
-  double* bl = reinterpret_cast<double*>(xb + NP);
-  if (li < NP) bl[li] = bd;
-  wave_sync();
-  double lt = 0.0;
-#pragma unroll
-  for (int k = 0; k < NP; ++k)
-    if (k >= li && li < NP) lt = fma(Lp[k * NP + li], bl[k], lt);
-  double c1 = act ? lt * lt : 0.0, c2 = act ? bd * bd : 0.0, c3 = act ? gi * bd : 0.0;
-#pragma unroll
-  for (int o = 1; o < 32; o <<= 1) {
-    c1 += __shfl_xor(c1, o, 32);
-    c2 += __shfl_xor(c2, o, 32);
-    c3 += __shfl_xor(c3, o, 32);
-  }
-  if (act) p.btop[(size_t(b) * kBetaSamples + s) * n + li] = beta;
-  if (sok && li == 0) p.bcost[size_t(b) * kBetaSamples + s] = float((c1 - delta * c2) - 2.0 * c3);
+}
+// sum over the quad, bit-identical in its 4 lanes
+DEVI double quad_sum(double v) {
+  v = v + dpp_d<0xB1>(v);  // quad_perm(1,0,3,2)
+  return v + dpp_d<0x4E>(v);  // quad_perm(2,3,0,1)
 }
 
-HDI int qp_np(int n) { return (n + 7) & ~7; }
-// per half-wave: L rows (NP x NP doubles), 1/L_jj (NP), solve hand-off (2 NP), beta (NP)
-HDI size_t qp_slot(int np) { return size_t(np) * np + 4 * np; }
-HDI size_t ker_qp_bytes(int n) { return size_t(2) * qp_slot(qp_np(n)) * 8; }
-
-__global__ __launch_bounds__(64) void k_bqp(Params p, int tb) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int np = qp_np(p.n), hw = threadIdx.x >> 5;
-  double* Lp = reinterpret_cast<double*>(smem) + size_t(hw) * qp_slot(np);
-  double* rinv = Lp + np * np;
-  switch (np) {
-    case 8: return bqp_solve<8>(p, Lp, rinv);
-    case 16: return bqp_solve<16>(p, Lp, rinv);
-    case 24: return bqp_solve<24>(p, Lp, rinv);
-    default: return bqp_solve<32>(p, Lp, rinv);
+template <int NP>
+DEVI void bqp_quad(const Params& p, int tb) {
+  constexpr int T4 = NP / 4;
+  const int n = p.n, M = p.M, q = threadIdx.x & 3;
+  const int s_lo = first_sample(tb), per = kBetaSamples - s_lo;
+  const int gq = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  const bool ok = gq < p.B * per;
+  const int gqc = ok ? gq : 0;
+  const int b = gqc / per, s = s_lo + gqc % per;
+  const int ntri = n * (n - 1) / 2;
+  const float* kr = p.bkred + (size_t(b) * kBetaSamples + s) * ntri;
+  const double* br = p.brow + (size_t(b) * kBetaSamples + s) * n;
+  const double inv_m = double(1.0f / float(M));
+  const double cdiag = double(1.0f + 0.05f);
+  const double delta = cdiag - 1.0;  // C_ii - K_ii (K_ii = exp(0) = 1)
+  // own rows: A[t][k] = C[4t+q][k], k <= 4t+3 (k > row: 0)
+  double A[T4][NP];
+  double g[T4], a1[T4], a2[T4], rin[T4];
+#pragma unroll
+  for (int t = 0; t < T4; ++t) {
+    const int i = 4 * t + q;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      if (k > 4 * t + 3) continue;
+      double v = 0.0;
+      if (k < i && i < n) v = double(kr[i * (i - 1) / 2 + k]);
+      if (k == i) v = i < n ? cdiag : 1.0;
+      A[t][k] = v;
+    }
+    g[t] = i < n ? br[i] * inv_m : 0.0;
+    a1[t] = g[t];
+    a2[t] = i < n ? 1.0 : 0.0;
+    rin[t] = 0.0;
   }
+  // Cholesky, column j
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const int tj = j >> 2, qj = j & 3;
+    const double sv = A[tj][j];
+    double y = __builtin_amdgcn_rsq(sv);  // 1/sqrt: v_rsq_f64 + two Newton steps
+    y = y * fma(-0.5 * sv, y * y, 1.5);
+    y = y * fma(-0.5 * sv, y * y, 1.5);
+    const double ry = quad_bcast(y, qj);
+    const double dj = sv * y;
+    if (q == qj) rin[tj] = y;
+#pragma unroll
+    for (int t = tj; t < T4; ++t) {
+      const double v = A[t][j] * ry;
+      A[t][j] = t > tj ? v : (q > qj ? v : (q == qj ? dj : 0.0));
+    }
+#pragma unroll
+    for (int k = j + 1; k < NP; ++k) {
+      const double lk = quad_bcast(A[k >> 2][j], k & 3);  // L_kj from the lane owning row k
+#pragma unroll
+      for (int t = k >> 2; t < T4; ++t) {
+        const double lij = (t == tj && q <= qj) ? 0.0 : A[t][j];
+        A[t][k] = fma(-lij, lk, A[t][k]);
+      }
+    }
+  }
+  // forward: L y = (g, 1)
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const int tj = j >> 2, qj = j & 3;
+    const double y1 = a1[tj] * rin[tj], y2 = a2[tj] * rin[tj];
+    if (q == qj) {
+      a1[tj] = y1;
+      a2[tj] = y2;
+    }
+    const double b1 = quad_bcast(y1, qj), b2 = quad_bcast(y2, qj);
+#pragma unroll
+    for (int t = tj; t < T4; ++t) {
+      const double lij = (t == tj && q <= qj) ? 0.0 : A[t][j];
+      a1[t] = fma(-lij, b1, a1[t]);
+      a2[t] = fma(-lij, b2, a2[t]);
+    }
+  }
+  // backward: L^T x = y (x overwrites y row by row, last row first)
+#pragma unroll
+  for (int j = NP - 1; j >= 0; --j) {
+    const int tj = j >> 2, qj = j & 3;
+    double p1 = 0.0, p2 = 0.0;
+#pragma unroll
+    for (int t = tj; t < T4; ++t) {
+      const double lij = (t == tj && q <= qj) ? 0.0 : A[t][j];
+      p1 = fma(lij, a1[t], p1);
+      p2 = fma(lij, a2[t], p2);
+    }
+    p1 = quad_sum(p1);
+    p2 = quad_sum(p2);
+    if (q == qj) {
+      a1[tj] = (a1[tj] - p1) * rin[tj];
+      a2[tj] = (a2[tj] - p2) * rin[tj];
+    }
+  }
+  double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int t = 0; t < T4; ++t) {
+    if (4 * t + q < n) {
+      s1 += a1[t];
+      s2 += a2[t];
+    }
+  }
+  s1 = quad_sum(s1);
+  s2 = quad_sum(s2);
+  const double alpha = (1.0 - s1) / s2;
+  float bf[T4];
+  double bd[T4];
+#pragma unroll
+  for (int t = 0; t < T4; ++t) {
+    bf[t] = 4 * t + q < n ? float(a1[t] + alpha * a2[t]) : 0.0f;
+    bd[t] = double(bf[t]);
+  }
+  // cost = |L^T beta|^2 - delta |beta|^2 - 2 g^T beta
+  double c1 = 0.0;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int ti = i >> 2, qi = i & 3;
+    double pi = 0.0;
+#pragma unroll
+    for (int t = ti; t < T4; ++t) {
+      const double lki = (t == ti && q < qi) ? 0.0 : A[t][i];
+      pi = fma(lki, bd[t], pi);
+    }
+    pi = quad_sum(pi);
+    c1 = fma(pi, pi, c1);
+  }
+  double c2 = 0.0, c3 = 0.0;
+#pragma unroll
+  for (int t = 0; t < T4; ++t) {
+    c2 = fma(bd[t], bd[t], c2);
+    c3 = fma(g[t], bd[t], c3);
+  }
+  c2 = quad_sum(c2);
+  c3 = quad_sum(c3);
+  if (!ok) return;
+  float* bt = p.btop + (size_t(b) * kBetaSamples + s) * n;
+#pragma unroll
+  for (int t = 0; t < T4; ++t)
+    if (4 * t + q < n) bt[4 * t + q] = bf[t];
+  if (q == 0) p.bcost[size_t(b) * kBetaSamples + s] = float((c1 - delta * c2) - 2.0 * c3);
+}
+
+HDI int qp_np(int n) { return n <= 8 ? 8 : (n <= 16 ? 16 : (n <= 24 ? 24 : 32)); }
+constexpr int kQpThreads = 256;  // 64 QPs per workgroup
+
+template <int NP>
+__global__ __launch_bounds__(kQpThreads) void k_bqp(Params p, int tb) {
+  bqp_quad<NP>(p, tb);
 }
 
 // ------------------------------------------------------------------------
 // k_belite: elites, mean, next generators; on the last iteration the outputs
 // (beta_best, sigma_best with the post-update quirk Q4, the reduced set).
 struct EliteLds {
-  size_t U, Gb, misc, total;
+  size_t U, Gb, misc, carry, total;
 };
 HDI EliteLds elite_lds(int M1) {
   EliteLds L{};
@@ -754,7 +820,8 @@ HDI EliteLds elite_lds(int M1) {
   L.U = 0;
   L.Gb = (size_t(M1) * 11 * 8 + 15) & ~size_t(15);
   L.misc = L.Gb + ((size_t(nblk) * 66 * 8 + 15) & ~size_t(15));
-  L.total = L.misc + 1024;
+  L.carry = L.misc + 1024;
+  L.total = L.carry + size_t(kBetaElite) * (2 * kMaxReduced + 2) * 4;
   return L;
 }
 
@@ -793,13 +860,41 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
   __syncthreads();
   const int imin = info[1] ? info[0] : elite[0];  // jnp.argmin: first NaN, else first minimum
   if (tid == 0) p.res_beta[size_t(b) * kBetaIters + tb] = info[1] ? __int_as_float(0x7fc00000) : cst[elite[0]];
+  // the elites are samples 0..10 of the next iteration, unchanged: carry
+  // their top-n rows, sigma, QP solution and cost there (first_sample)
+  if (tb < kBetaIters - 1) {
+    int* csel = reinterpret_cast<int*>(smem + C.carry);
+    float* ctop = reinterpret_cast<float*>(csel + kBetaElite * n);
+    float* csig = ctop + kBetaElite * n;
+    float* ccost = csig + kBetaElite;
+    const size_t rb = size_t(b) * kBetaSamples;
+    for (int i = tid; i < kBetaElite * n; i += blockDim.x) {
+      const int q = i / n, k = i - q * n;
+      const size_t src = (rb + elite[q]) * n + k;
+      csel[i] = p.bsel[src];
+      ctop[i] = p.btop[src];
+    }
+    if (tid < kBetaElite) {
+      csig[tid] = p.bsig[rb + elite[tid]];
+      ccost[tid] = cst[elite[tid]];
+    }
+    __syncthreads();
+    for (int i = tid; i < kBetaElite * n; i += blockDim.x) {
+      p.bsel[rb * n + i] = csel[i];
+      p.btop[rb * n + i] = ctop[i];
+    }
+    if (tid < kBetaElite) {
+      p.bsig[rb + tid] = csig[tid];
+      p.bcost[rb + tid] = ccost[tid];
+    }
+  }
   // ---- E_new = the 11 elite sample vectors (rows 0..10 of the next samples):
   // previous elites, this iteration's new samples (ygen), or at tb = 0 the
   // initial samples
   const float* Eold = p.belite + (size_t(tb & 1) * p.B + b) * kBetaElite * M1;
   float* Enew = p.belite + (size_t((tb + 1) & 1) * p.B + b) * kBetaElite * M1;
   const int ys = ygen_stride(M);
-  const float* Y = p.ygen + size_t(b) * kNew * ys;
+  const float* Y = p.ygen + size_t(b) * kBzCols * ys;
   for (int i = tid; i < kBetaElite * M1; i += blockDim.x) {
     const int q = i / M1, j = i - q * M1;
     const int e = elite[q];
@@ -819,13 +914,13 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
   const bool last = tb == kBetaIters - 1;
   // ---- mean, U = (E - mean) / sqrt(10), generators of the next iteration
   const double rs10 = 1.0 / sqrt(10.0);
-  double* gen = p.gen + size_t(b) * M1 * kGenStride;
+  double* gen = p.gen + size_t(b) * pos_pad(M) * kGenStride;
   for (int j = tid; j < M1; j += blockDim.x) {
     double s = 0.0;
     for (int q = 0; q < kBetaElite; ++q) s = s + double(Enew[size_t(q) * M1 + j]);
     const double m = s / double(kBetaElite);
     for (int q = 0; q < kBetaElite; ++q) Ul[j * 11 + q] = (double(Enew[size_t(q) * M1 + j]) - m) * rs10;
-    p.genm[size_t(b) * M1 + j] = float(m);
+    p.genm[size_t(b) * pos_pad(M) + j] = float(m);
   }
   __syncthreads();
   // level 1: block sums of u u^T over 16 positions (66 packed entries)
@@ -942,13 +1037,13 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
     // sigma coordinate of new sample imin-11 drawn with the NEW generators:
     // y_M = mean_M + L_MM z_M + u_M . sum_{j<M} w_j z_j
     double* red = reinterpret_cast<double*>(smem + C.Gb);  // reuse
-    const float* z = p.beta_z + size_t(tb) * M1 * kNew;
+    const float* z = p.beta_z + size_t(tb) * pos_pad(M) * kBzCols;
     const int si = imin - kBetaElite;
     double part[11];
 #pragma unroll
     for (int a = 0; a < 11; ++a) part[a] = 0.0;
     for (int j = tid; j < M; j += blockDim.x) {
-      const double zj = double(z[size_t(j) * kNew + si]);
+      const double zj = double(z[size_t(j) * kBzCols + si]);
 #pragma unroll
       for (int a = 0; a < 11; ++a) part[a] += gen[size_t(j) * kGenStride + a] * zj;
     }
@@ -969,8 +1064,8 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
         for (int w2 = 0; w2 < (int)(blockDim.x >> 6); ++w2) sa += red[w2 * 11 + a];
         d += g[11 + a] * sa;
       }
-      const double zM = double(z[size_t(M) * kNew + si]);
-      const float yM = float((double(p.genm[size_t(b) * M1 + M]) + g[22] * zM) + d);
+      const double zM = double(z[size_t(M) * kBzCols + si]);
+      const float yM = float((double(p.genm[size_t(b) * pos_pad(M) + M]) + g[22] * zM) + d);
       p.sigma[b] = fmaxf(yM, 0.01f);
     }
   }
@@ -1036,10 +1131,6 @@ bool mmdopt_supported(int n, int H, int O, std::string* why) {
     return false;
   }
   const EliteLds e = elite_lds(M + 1);
-  if (bs_lds(M + 1) > kLdsBudget) {
-    if (why) *why = "mmd_opt: num_reduced^2 too large for the sampling stage";
-    return false;
-  }
   if (e.total > kLdsBudget) {
     if (why) *why = "mmd_opt: num_reduced^2 too large for the elite stage";
     return false;
@@ -1053,8 +1144,12 @@ void launch_mother(const Params& p, int t, hipStream_t s) {
   hipLaunchKernelGGL(k_mother, dim3(p.B), dim3(kThreads), size_t(2) * p.n * p.H * 4, s, p, t);
 }
 
+void launch_bdist(const Params& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_bdist, dim3(p.B, (p.M + kDistRows - 1) / kDistRows), dim3(kDistThreads), 0, s, p);
+}
+
 void launch_bsample(const Params& p, int tb, hipStream_t s) {
-  hipLaunchKernelGGL(k_bsample, dim3(p.B), dim3(kThreads), bs_lds(p.M + 1), s, p, tb);
+  hipLaunchKernelGGL(k_bsample, dim3(p.B), dim3(64 * kSampleWaves), 0, s, p, tb);
 }
 
 void launch_bselect(const Params& p, int tb, hipStream_t s) {
@@ -1062,7 +1157,22 @@ void launch_bselect(const Params& p, int tb, hipStream_t s) {
 }
 
 void launch_bqp(const Params& p, int tb, hipStream_t s) {
-  hipLaunchKernelGGL(k_bqp, dim3(p.B, kBetaSamples / 2), dim3(64), ker_qp_bytes(p.n), s, p, tb);
+  const int qps = p.B * (kBetaSamples - first_sample(tb));
+  const dim3 grid((qps * 4 + kQpThreads - 1) / kQpThreads);
+  switch (qp_np(p.n)) {
+    case 8:
+      hipLaunchKernelGGL((k_bqp<8>), grid, dim3(kQpThreads), 0, s, p, tb);
+      return;
+    case 16:
+      hipLaunchKernelGGL((k_bqp<16>), grid, dim3(kQpThreads), 0, s, p, tb);
+      return;
+    case 24:
+      hipLaunchKernelGGL((k_bqp<24>), grid, dim3(kQpThreads), 0, s, p, tb);
+      return;
+    default:
+      hipLaunchKernelGGL((k_bqp<32>), grid, dim3(kQpThreads), 0, s, p, tb);
+      return;
+  }
 }
 
 void launch_bkernel(const Params& p, int tb, hipStream_t s) {

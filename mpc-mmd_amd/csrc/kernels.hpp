@@ -20,6 +20,13 @@ constexpr int kElite = 5;              // cem.py:138
 constexpr int kResultStride = 11 + 11 + 2 + 1 + 20 + kMaxReduced;  // cx, cy, lane, obs, sigma, res_beta, beta
 constexpr int kGenStride = 24;         // doubles per position in Params::gen
 HDI_CONST int ygen_stride(int M) { return ((M + 1) + 31) & ~31; }
+// beta-CEM sample generation works on blocks of 16 positions and tiles of 16
+// samples: generators (gen, genm) and the device normals (beta_z) are padded
+// with zeros to pos_pad(M) positions, beta_z rows and ygen to kBzCols samples
+constexpr int kBzCols = 96;
+HDI_CONST int pos_pad(int M) { return ((M + 1) + 15) & ~15; }
+// row stride (floats) of the mother distance matrix; pad columns hold +inf
+HDI_CONST int dist_stride(int M) { return (M + 3) & ~3; }
 
 struct Params {
   // shapes / configuration
@@ -43,7 +50,7 @@ struct Params {
   const float* roll;       // [T][3][H][S]
   const float* resample;   // [T][B-5][8]
   const float* beta_z0;    // [100][M+1]
-  const float* beta_z;     // [20][89][M+1]
+  const float* beta_z;     // [20][pos_pad(M)][kBzCols] (position-major, zero padded)
   // carry / state
   float* pop;              // [2][B][8] double-buffered population
   float* mean;             // [8]
@@ -65,22 +72,24 @@ struct Params {
   float* res_beta;         // [B][20]
   // mmd_opt scratch (beta-CEM, compute_beta.py:93-157)
   float* feat;             // [B][22][M]   mother Bernstein coefficients (cx | cy)
+  float* bdist;            // [B][M][dist_stride(M)] L1 distances of the mother features
+                           //              (kernel_computation.py:33-39), once per outer iteration
   float* ctrl_n;           // [B][2][n][H] noisy control rows (acc, steer)
   int32_t* bsel;           // [B][100][n]  top-n |beta| indices (argsort order)
   float* bsig;             // [B][100]     sample sigma (last coordinate, clipped)
   float* btop;             // [B][100][n]  QP solutions
   float* bcost;            // [B][100]     QP costs
   float* belite;           // [2][B][11][M+1] elite sample vectors (ping-pong)
-  double* gen;             // [B][M+1][kGenStride] W (11), U (11), L_jj
-  float* genm;             // [B][M+1]     float32 elite mean
+  double* gen;             // [B][pos_pad(M)][kGenStride] W (11), U (11), L_jj (pad rows 0)
+  float* genm;             // [B][pos_pad(M)]  float32 elite mean (pad 0)
   int32_t* bestsel;        // [B][n]       reduced set of the best sample
   double* brow;            // [B][100][n]  K_mixed row sums (fp64)
   float* bkred;            // [B][100][n(n-1)/2] K_red strict lower triangle
-  float* ygen;             // [B][89][ygs] new samples of the current beta-iteration (ygs = M+1 rounded to 32)
+  float* ygen;             // [B][kBzCols][ygs] new samples of the current beta-iteration (ygs = M+1 rounded to 32)
   // phase timestamps (s_memrealtime, 100 MHz) of workgroup 0, for profiling
   unsigned long long* dbg;  // [64]
-  // work counters for the roofline: [0] sum over k_bkernel workgroups of the
-  // distinct mother rows (distance rows computed)
+  // work counters for the roofline, summed over k_bkernel workgroups:
+  // [0] distinct distance rows staged, [1] (sample, reduced row) pairs summed
   unsigned long long* stats;  // [8]
   // outputs
   float* results;          // [T][kResultStride]
@@ -95,6 +104,7 @@ void launch_select(const Params& p, int t, hipStream_t s);
 void launch_risk_baseline(const Params& p, int t, hipStream_t s);
 // mmd_opt risk, one launch each (mpcmmd.hip chains them)
 void launch_mother(const Params& p, int t, hipStream_t s);
+void launch_bdist(const Params& p, hipStream_t s);
 void launch_bsample(const Params& p, int tb, hipStream_t s);
 void launch_bselect(const Params& p, int tb, hipStream_t s);
 void launch_bkernel(const Params& p, int tb, hipStream_t s);

@@ -45,6 +45,7 @@ enum KernelId {
   kKFront,
   kKRiskBaseline,
   kKMother,
+  kKBDist,
   kKBSample,
   kKBSelect,
   kKBKernel,
@@ -54,8 +55,8 @@ enum KernelId {
   kKSelect,
   kNumKernels
 };
-const char* kKernelNames[kNumKernels] = {"noise",   "front", "risk_baseline", "mother", "bsample", "bselect",
-                                         "bkernel", "bqp",   "belite",        "mmdfinal", "select"};
+const char* kKernelNames[kNumKernels] = {"noise",   "front", "risk_baseline", "mother",   "bdist", "bsample",
+                                         "bselect", "bkernel", "bqp",         "belite", "mmdfinal", "select"};
 
 }  // namespace
 
@@ -167,13 +168,14 @@ void upload(mpcmmd_handle* h, const char* name, const void* src, size_t bytes, s
   HIPC(hipMemcpyAsync(static_cast<char*>(it->second.first) + offset, src, bytes, hipMemcpyHostToDevice, h->stream));
 }
 
-// beta_z iteration t: [89][M+1] (draw order) -> device [M+1][89], so the
-// generation kernels read one position for 64 samples in one transaction
+// beta_z iteration t: [89][M+1] (draw order) -> device [pos_pad(M)][kBzCols]
+// (position-major, zero padded), so the generation kernel reads one position
+// for 16 samples in one transaction and whole 16 x 16 blocks without bounds
 void upload_beta_z(mpcmmd_handle* h, int t, const float* z) {
   const int M1 = h->M + 1, R = kBetaSamples - kBetaElite;
-  std::vector<float> tr(size_t(R) * M1);
+  std::vector<float> tr(size_t(pos_pad(h->M)) * kBzCols, 0.0f);
   for (int r = 0; r < R; ++r)
-    for (int j = 0; j < M1; ++j) tr[size_t(j) * R + r] = z[size_t(r) * M1 + j];
+    for (int j = 0; j < M1; ++j) tr[size_t(j) * kBzCols + r] = z[size_t(r) * M1 + j];
   upload(h, "beta_z", tr.data(), tr.size() * 4, size_t(t) * tr.size() * 4);
   HIPC(hipStreamSynchronize(h->stream));  // tr is a host temporary
 }
@@ -214,6 +216,7 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
       if (p.cost == MPCMMD_COST_MMD_OPT) {
         if (!h->mmd_ok) throw std::invalid_argument("mmd_opt unsupported for this configuration: " + h->mmd_why);
         h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
+        h->launch(kKBDist, [&] { launch_bdist(p, h->stream); });
         for (int tb = 0; tb < kBetaIters; ++tb) run_beta_iteration(h, tb);
         h->launch(kKMmdFinal, [&] { launch_mmdfinal(p, t, h->stream); });
       } else
@@ -229,7 +232,10 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
     case 8:
       if (p.cost != MPCMMD_COST_MMD_OPT || !h->mmd_ok) throw std::invalid_argument("stages 4-8 need cost mmd_opt");
       if (stage >= 5 && stage <= 7 && t >= kBetaIters) throw std::invalid_argument("beta-CEM iteration out of range");
-      if (stage == 4) h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
+      if (stage == 4) {  // mother rollouts, features and their distance matrix
+        h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
+        h->launch(kKBDist, [&] { launch_bdist(p, h->stream); });
+      }
       if (stage == 5) {  // samples + their top-n rows
         if (t > 0) h->launch(kKBSample, [&] { launch_bsample(p, t, h->stream); });
         h->launch(kKBSelect, [&] { launch_bselect(p, t, h->stream); });
@@ -361,21 +367,23 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
     p.resample = (const float*)h->alloc("resample", size_t(T) * (B - kElite) * 8 * 4);
     if (mmd_ok) {
       p.beta_z0 = (const float*)h->alloc("beta_z0", size_t(kBetaSamples) * (h->M + 1) * 4);
-      p.beta_z = (const float*)h->alloc("beta_z", size_t(kBetaIters) * (kBetaSamples - kBetaElite) * (h->M + 1) * 4);
+      p.beta_z = (const float*)h->alloc("beta_z", size_t(kBetaIters) * pos_pad(h->M) * kBzCols * 4);
       const size_t M = h->M, M1 = M + 1, n = h->n;
       p.feat = (float*)h->alloc("feat", size_t(B) * 22 * M * 4);
+      p.bdist = (float*)h->alloc("bdist", size_t(B) * M * dist_stride(int(M)) * 4);
       p.ctrl_n = (float*)h->alloc("ctrl_n", size_t(B) * 2 * n * H * 4);
       p.bsel = (int32_t*)h->alloc("bsel", size_t(B) * kBetaSamples * n * 4);
       p.bsig = (float*)h->alloc("bsig", size_t(B) * kBetaSamples * 4);
       p.btop = (float*)h->alloc("btop", size_t(B) * kBetaSamples * n * 4);
       p.bcost = (float*)h->alloc("bcost", size_t(B) * kBetaSamples * 4);
       p.belite = (float*)h->alloc("belite", size_t(2) * B * kBetaElite * M1 * 4);
-      p.gen = (double*)h->alloc("gen", size_t(B) * M1 * kGenStride * 8);
-      p.genm = (float*)h->alloc("genm", size_t(B) * M1 * 4);
+      const size_t Pp = pos_pad(h->M);
+      p.gen = (double*)h->alloc("gen", size_t(B) * Pp * kGenStride * 8);
+      p.genm = (float*)h->alloc("genm", size_t(B) * Pp * 4);
       p.bestsel = (int32_t*)h->alloc("bestsel", size_t(B) * n * 4);
       p.brow = (double*)h->alloc("brow", size_t(B) * kBetaSamples * n * 8);
       p.bkred = (float*)h->alloc("bkred", size_t(B) * kBetaSamples * (n * (n - 1) / 2) * 4);
-      p.ygen = (float*)h->alloc("ygen", size_t(B) * (kBetaSamples - kBetaElite) * ygen_stride(h->M) * 4);
+      p.ygen = (float*)h->alloc("ygen", size_t(B) * kBzCols * ygen_stride(h->M) * 4);
     }
     p.pop = (float*)h->alloc("pop", size_t(2) * B * 8 * 4);
     p.mean = (float*)h->alloc("mean", 8 * 4);

@@ -63,7 +63,37 @@ __global__ void k_probe(unsigned long long* out, double* sink, int iters) {
   }
   t1 = __builtin_amdgcn_s_memtime();
   if (lane == 0) out[5] = t1 - t0;
-  sink[lane] = x + idx + acc + v + a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+  // independent f64 MFMA 16x16x4 (throughput, 4 accumulators)
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  d4 c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
+  const double fa = 1e-3 * lane, fb = 2e-3 * lane;
+  t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < iters; ++i) {
+    c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, fb, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(fb, fa, c1, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, fa, c2, 0, 0, 0);
+    c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(fb, fb, c3, 0, 0, 0);
+  }
+  t1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) out[6] = t1 - t0;
+  // dependent f64 MFMA chain (one accumulator)
+  d4 e0 = {0, 0, 0, 0};
+  t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < iters; ++i) e0 = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, fb, e0, 0, 0, 0);
+  t1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) out[7] = t1 - t0;
+  // independent v_exp_f32 (8 chains)
+  float q0 = lane * -1e-3f, q1 = q0 - 1, q2 = q0 - 2, q3 = q0 - 3, q4 = q0 - 4, q5 = q0 - 5, q6 = q0 - 6, q7 = q0 - 7;
+  t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < iters; ++i) {
+    q0 = __builtin_amdgcn_exp2f(q0); q1 = __builtin_amdgcn_exp2f(q1); q2 = __builtin_amdgcn_exp2f(q2);
+    q3 = __builtin_amdgcn_exp2f(q3); q4 = __builtin_amdgcn_exp2f(q4); q5 = __builtin_amdgcn_exp2f(q5);
+    q6 = __builtin_amdgcn_exp2f(q6); q7 = __builtin_amdgcn_exp2f(q7);
+  }
+  t1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) out[8] = t1 - t0;
+  sink[lane] = x + idx + acc + v + a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + c0[0] + c1[1] + c2[2] + c3[3] + e0[0] +
+               q0 + q1 + q2 + q3 + q4 + q5 + q6 + q7;
 }
 
 int main() {
@@ -76,13 +106,16 @@ int main() {
     hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, 0, d, s, iters);
     (void)hipDeviceSynchronize();
   }
-  unsigned long long h[8];
-  (void)hipMemcpy(h, d, 6 * 8, hipMemcpyDeviceToHost);
+  unsigned long long h[16];
+  (void)hipMemcpy(h, d, 9 * 8, hipMemcpyDeviceToHost);
   std::printf("clock: %llu cycles in %llu ticks of 100 MHz -> %.2f GHz\n", h[0], h[1], h[0] / (h[1] * 10.0));
   std::printf("dependent fp64 fma: %.1f cycles\n", double(h[0]) / iters);
   std::printf("dependent LDS load (+cvt): %.1f cycles\n", double(h[2]) / iters);
   std::printf("4x ballot+popc step: %.1f cycles\n", double(h[3]) / iters);
   std::printf("readlane fp64 bcast step: %.1f cycles\n", double(h[4]) / iters);
   std::printf("8 independent fp64 fma: %.1f cycles\n", double(h[5]) / iters);
+  std::printf("4 independent f64 mfma 16x16x4: %.1f cycles\n", double(h[6]) / iters);
+  std::printf("dependent f64 mfma 16x16x4: %.1f cycles\n", double(h[7]) / iters);
+  std::printf("8 independent v_exp_f32: %.1f cycles\n", double(h[8]) / iters);
   return 0;
 }
