@@ -328,28 +328,67 @@ struct SampleBlock {
   double z[kTilesPerWave][4];  // Z[p0 + 4k + h][s0 + 16t + r]
 };
 
-DEVI void load_block(SampleBlock& q, const double* G, const float* gm, const float* z, int p0, int s0, int r,
+DEVI void load_block(SampleBlock& q, const double* G, const double* gm, const double* z, int p0, int s0, int r,
                      int h) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const double v = G[size_t(p0 + 4 * k + h) * kGenStride + r];
-    q.wA[k] = r < 11 ? v : 0.0;
-  }
+  for (int k = 0; k < 4; ++k) q.wA[k] = G[size_t(p0 + 4 * k + h) * kGenStride + kGenW + r];  // rows >= 11 of S unused
   const double* g = G + size_t(p0 + r) * kGenStride;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    const int f = 4 * i + h;
-    const double vw = g[f], vu = g[11 + f];
-    q.wX[i] = f < 11 ? vw : 0.0;
-    q.uX[i] = f < 11 ? vu : 0.0;
+    q.wX[i] = g[kGenW + 4 * i + h];  // feature 11 reads a zero slot
+    q.uX[i] = g[kGenU + 4 * i + h];
   }
-  q.L = g[22];
+  q.L = g[kGenL];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) q.m[i] = double(gm[p0 + h + 4 * i]);
+  for (int i = 0; i < 4; ++i) q.m[i] = gm[p0 + h + 4 * i];
 #pragma unroll
   for (int t = 0; t < kTilesPerWave; ++t)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) q.z[t][k] = double(z[size_t(p0 + 4 * k + h) * kBzCols + s0 + 16 * t + r]);
+    for (int k = 0; k < 4; ++k) q.z[t][k] = z[size_t(p0 + 4 * k + h) * kBzCols + s0 + 16 * t + r];
+}
+
+// one block: Y = m + T Z + U S for the wave's tiles, then S += W^T Z
+DEVI void sample_block(const SampleBlock& cur, d4* S, float* Y, int p0, int M, int ys, int r, int h) {
+  // X = W_c U_c^T: register i holds w_{h+4i} . u_r = T[row r][col h + 4i]
+  d4 X = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) X = mfma64(cur.wX[i], cur.uX[i], X);
+  double T[4];  // A operand of T Z, k-step i: T[r][4i + h]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = h + 4 * i;
+    T[i] = k < r ? X[i] : (k == r ? cur.L : 0.0);
+  }
+  // independent chains, tiles interleaved: Y = m + T Z (acc a) + U S (acc b),
+  // P = W^T Z (two partial accumulators), S += P after U S has read S
+  d4 Ya[kTilesPerWave], Yb[kTilesPerWave], P0[kTilesPerWave], P1[kTilesPerWave];
+#pragma unroll
+  for (int t = 0; t < kTilesPerWave; ++t) {
+    Ya[t] = d4{cur.m[0], cur.m[1], cur.m[2], cur.m[3]};
+    Yb[t] = d4{0.0, 0.0, 0.0, 0.0};
+    P0[t] = d4{0.0, 0.0, 0.0, 0.0};
+    P1[t] = d4{0.0, 0.0, 0.0, 0.0};
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int t = 0; t < kTilesPerWave; ++t) {
+      if (k < 3) Yb[t] = mfma64(cur.uX[k], S[t][k], Yb[t]);
+      if (k & 1) P1[t] = mfma64(cur.wA[k], cur.z[t][k], P1[t]);
+      else P0[t] = mfma64(cur.wA[k], cur.z[t][k], P0[t]);
+    }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int t = 0; t < kTilesPerWave; ++t) Ya[t] = mfma64(T[k], cur.z[t][k], Ya[t]);
+#pragma unroll
+  for (int t = 0; t < kTilesPerWave; ++t) {
+    S[t] = S[t] + (P0[t] + P1[t]);
+    const d4 Yv = Ya[t] + Yb[t];
+    float* yrow = Y + size_t(16 * t) * ys + p0 + h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) yrow[4 * i] = p0 + h + 4 * i == M ? fmaxf(float(Yv[i]), 0.01f) : float(Yv[i]);
+  }
 }
 
 __global__ __launch_bounds__(64 * kSampleWaves) void k_bsample(Params p, int tb) {
@@ -359,58 +398,29 @@ __global__ __launch_bounds__(64 * kSampleWaves) void k_bsample(Params p, int tb)
   const int s0 = w * kTilesPerWave * 16;
   MPCMMD_STAMP(p, 0);
   const double* G = p.gen + size_t(b) * Pp * kGenStride;
-  const float* gm = p.genm + size_t(b) * Pp;
-  const float* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
+  const double* gm = p.genm + size_t(b) * Pp;
+  const double* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
   const int ys = ygen_stride(M);
   float* Y = p.ygen + (size_t(b) * kBzCols + s0 + r) * ys;
   d4 S[kTilesPerWave];
 #pragma unroll
   for (int t = 0; t < kTilesPerWave; ++t) S[t] = d4{0.0, 0.0, 0.0, 0.0};
   const int nblk = Pp >> 4;
-  SampleBlock cur;
-  load_block(cur, G, gm, z, 0, s0, r, h);
-  for (int c = 0; c < nblk; ++c) {
+  // blocks in pairs, operands ping-ponged: the next block's loads are in
+  // flight while this block's MFMAs run (the last prefetch re-reads a block)
+  // (nblk is even; sched barriers keep the prefetch ahead of the MFMAs)
+  SampleBlock qa, qb;
+  load_block(qa, G, gm, z, 0, s0, r, h);
+  for (int c = 0; c < nblk; c += 2) {
     const int p0 = c << 4;
-    SampleBlock nxt;
-    load_block(nxt, G, gm, z, min(p0 + 16, Pp - 16), s0, r, h);  // prefetch (last block: reload)
-    // X = W_c U_c^T: register i holds w_{h+4i} . u_r = T[row r][col h + 4i]
-    d4 X = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int i = 0; i < 3; ++i) X = mfma64(cur.wX[i], cur.uX[i], X);
-    double T[4];  // A operand of T Z, k-step i: T[r][4i + h]
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = h + 4 * i;
-      T[i] = k < r ? X[i] : (k == r ? cur.L : 0.0);
-    }
-    // independent chains, tiles interleaved: Y = m + T Z (acc a) + U S (acc b),
-    // P = W^T Z (two partial accumulators), S += P after U S has read S
-    d4 Ya[kTilesPerWave], Yb[kTilesPerWave], P0[kTilesPerWave], P1[kTilesPerWave];
-#pragma unroll
-    for (int t = 0; t < kTilesPerWave; ++t) {
-      Ya[t] = d4{cur.m[0], cur.m[1], cur.m[2], cur.m[3]};
-      Yb[t] = d4{0.0, 0.0, 0.0, 0.0};
-      P0[t] = d4{0.0, 0.0, 0.0, 0.0};
-      P1[t] = d4{0.0, 0.0, 0.0, 0.0};
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int t = 0; t < kTilesPerWave; ++t) {
-        if (k < 3) Yb[t] = mfma64(cur.uX[k], S[t][k], Yb[t]);
-        if (k & 1) P1[t] = mfma64(cur.wA[k], cur.z[t][k], P1[t]);
-        else P0[t] = mfma64(cur.wA[k], cur.z[t][k], P0[t]);
-        Ya[t] = mfma64(T[k], cur.z[t][k], Ya[t]);
-      }
-#pragma unroll
-    for (int t = 0; t < kTilesPerWave; ++t) {
-      S[t] = S[t] + (P0[t] + P1[t]);
-      const d4 Yv = Ya[t] + Yb[t];
-      float* yrow = Y + size_t(16 * t) * ys + p0 + h;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) yrow[4 * i] = p0 + h + 4 * i == M ? fmaxf(float(Yv[i]), 0.01f) : float(Yv[i]);
-    }
-    cur = nxt;
+    load_block(qb, G, gm, z, p0 + 16, s0, r, h);
+    __builtin_amdgcn_sched_barrier(0);
+    sample_block(qa, S, Y, p0, M, ys, r, h);
+    __builtin_amdgcn_sched_barrier(0);
+    load_block(qa, G, gm, z, min(p0 + 32, Pp - 16), s0, r, h);
+    __builtin_amdgcn_sched_barrier(0);
+    sample_block(qb, S, Y, p0 + 16, M, ys, r, h);
+    __builtin_amdgcn_sched_barrier(0);
   }
   MPCMMD_STAMP(p, 1);
 }
@@ -920,7 +930,7 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
     for (int q = 0; q < kBetaElite; ++q) s = s + double(Enew[size_t(q) * M1 + j]);
     const double m = s / double(kBetaElite);
     for (int q = 0; q < kBetaElite; ++q) Ul[j * 11 + q] = (double(Enew[size_t(q) * M1 + j]) - m) * rs10;
-    p.genm[size_t(b) * pos_pad(M) + j] = float(m);
+    p.genm[size_t(b) * pos_pad(M) + j] = double(float(m));
   }
   __syncthreads();
   // level 1: block sums of u u^T over 16 positions (66 packed entries)
@@ -1017,10 +1027,10 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
     double* g = gen + size_t(j) * kGenStride;
 #pragma unroll
     for (int a = 0; a < 11; ++a) {
-      g[a] = v[a] * rl;
-      g[11 + a] = u[a];
+      g[kGenW + a] = v[a] * rl;
+      g[kGenU + a] = u[a];
     }
-    g[22] = ljj;
+    g[kGenL] = ljj;
   }
   if (!last) return;
   __syncthreads();
@@ -1037,15 +1047,15 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
     // sigma coordinate of new sample imin-11 drawn with the NEW generators:
     // y_M = mean_M + L_MM z_M + u_M . sum_{j<M} w_j z_j
     double* red = reinterpret_cast<double*>(smem + C.Gb);  // reuse
-    const float* z = p.beta_z + size_t(tb) * pos_pad(M) * kBzCols;
+    const double* z = p.beta_z + size_t(tb) * pos_pad(M) * kBzCols;
     const int si = imin - kBetaElite;
     double part[11];
 #pragma unroll
     for (int a = 0; a < 11; ++a) part[a] = 0.0;
     for (int j = tid; j < M; j += blockDim.x) {
-      const double zj = double(z[size_t(j) * kBzCols + si]);
+      const double zj = z[size_t(j) * kBzCols + si];
 #pragma unroll
-      for (int a = 0; a < 11; ++a) part[a] += gen[size_t(j) * kGenStride + a] * zj;
+      for (int a = 0; a < 11; ++a) part[a] += gen[size_t(j) * kGenStride + kGenW + a] * zj;
     }
 #pragma unroll
     for (int a = 0; a < 11; ++a) {
@@ -1062,10 +1072,10 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
       for (int a = 0; a < 11; ++a) {
         double sa = 0.0;
         for (int w2 = 0; w2 < (int)(blockDim.x >> 6); ++w2) sa += red[w2 * 11 + a];
-        d += g[11 + a] * sa;
+        d += g[kGenU + a] * sa;
       }
-      const double zM = double(z[size_t(M) * kBzCols + si]);
-      const float yM = float((double(p.genm[size_t(b) * pos_pad(M) + M]) + g[22] * zM) + d);
+      const double zM = z[size_t(M) * kBzCols + si];
+      const float yM = float((p.genm[size_t(b) * pos_pad(M) + M] + g[kGenL] * zM) + d);
       p.sigma[b] = fmaxf(yM, 0.01f);
     }
   }

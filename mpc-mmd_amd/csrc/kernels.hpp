@@ -18,13 +18,18 @@ constexpr int kBetaElite = 11;         // compute_beta.py:26
 constexpr int kEliteCost = 20;         // cem.py:140
 constexpr int kElite = 5;              // cem.py:138
 constexpr int kResultStride = 11 + 11 + 2 + 1 + 20 + kMaxReduced;  // cx, cy, lane, obs, sigma, res_beta, beta
-constexpr int kGenStride = 24;         // doubles per position in Params::gen
+// doubles per position in Params::gen: W 0..10, zeros 11..14, L_jj 15,
+// U 16..26, zeros 27..31 (the zero slots are the padding features of the
+// 16x16x4 MFMA operands, so the sampling kernel loads them unmasked)
+constexpr int kGenStride = 32;
+constexpr int kGenW = 0, kGenL = 15, kGenU = 16;
 HDI_CONST int ygen_stride(int M) { return ((M + 1) + 31) & ~31; }
-// beta-CEM sample generation works on blocks of 16 positions and tiles of 16
-// samples: generators (gen, genm) and the device normals (beta_z) are padded
-// with zeros to pos_pad(M) positions, beta_z rows and ygen to kBzCols samples
+// beta-CEM sample generation works on pairs of blocks of 16 positions and
+// tiles of 16 samples: generators (gen, genm) and the device normals (beta_z)
+// are padded with zeros to pos_pad(M) positions, beta_z rows and ygen to
+// kBzCols samples
 constexpr int kBzCols = 96;
-HDI_CONST int pos_pad(int M) { return ((M + 1) + 15) & ~15; }
+HDI_CONST int pos_pad(int M) { return ((M + 1) + 31) & ~31; }  // whole pairs of 16-blocks
 // row stride (floats) of the mother distance matrix; pad columns hold +inf
 HDI_CONST int dist_stride(int M) { return (M + 3) & ~3; }
 
@@ -50,7 +55,7 @@ struct Params {
   const float* roll;       // [T][3][H][S]
   const float* resample;   // [T][B-5][8]
   const float* beta_z0;    // [100][M+1]
-  const float* beta_z;     // [20][pos_pad(M)][kBzCols] (position-major, zero padded)
+  const double* beta_z;    // [20][pos_pad(M)][kBzCols] fp32 normals held as fp64 (position-major, zero padded)
   // carry / state
   float* pop;              // [2][B][8] double-buffered population
   float* mean;             // [8]
@@ -80,8 +85,8 @@ struct Params {
   float* btop;             // [B][100][n]  QP solutions
   float* bcost;            // [B][100]     QP costs
   float* belite;           // [2][B][11][M+1] elite sample vectors (ping-pong)
-  double* gen;             // [B][pos_pad(M)][kGenStride] W (11), U (11), L_jj (pad rows 0)
-  float* genm;             // [B][pos_pad(M)]  float32 elite mean (pad 0)
+  double* gen;             // [B][pos_pad(M)][kGenStride] W, L_jj, U (pad rows 0)
+  double* genm;            // [B][pos_pad(M)]  fp32-rounded elite mean, as fp64 (pad 0)
   int32_t* bestsel;        // [B][n]       reduced set of the best sample
   double* brow;            // [B][100][n]  K_mixed row sums (fp64)
   float* bkred;            // [B][100][n(n-1)/2] K_red strict lower triangle

@@ -173,10 +173,10 @@ void upload(mpcmmd_handle* h, const char* name, const void* src, size_t bytes, s
 // for 16 samples in one transaction and whole 16 x 16 blocks without bounds
 void upload_beta_z(mpcmmd_handle* h, int t, const float* z) {
   const int M1 = h->M + 1, R = kBetaSamples - kBetaElite;
-  std::vector<float> tr(size_t(pos_pad(h->M)) * kBzCols, 0.0f);
+  std::vector<double> tr(size_t(pos_pad(h->M)) * kBzCols, 0.0);
   for (int r = 0; r < R; ++r)
-    for (int j = 0; j < M1; ++j) tr[size_t(j) * kBzCols + r] = z[size_t(r) * M1 + j];
-  upload(h, "beta_z", tr.data(), tr.size() * 4, size_t(t) * tr.size() * 4);
+    for (int j = 0; j < M1; ++j) tr[size_t(j) * kBzCols + r] = double(z[size_t(r) * M1 + j]);
+  upload(h, "beta_z", tr.data(), tr.size() * 8, size_t(t) * tr.size() * 8);
   HIPC(hipStreamSynchronize(h->stream));  // tr is a host temporary
 }
 
@@ -367,7 +367,7 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
     p.resample = (const float*)h->alloc("resample", size_t(T) * (B - kElite) * 8 * 4);
     if (mmd_ok) {
       p.beta_z0 = (const float*)h->alloc("beta_z0", size_t(kBetaSamples) * (h->M + 1) * 4);
-      p.beta_z = (const float*)h->alloc("beta_z", size_t(kBetaIters) * pos_pad(h->M) * kBzCols * 4);
+      p.beta_z = (const double*)h->alloc("beta_z", size_t(kBetaIters) * pos_pad(h->M) * kBzCols * 8);
       const size_t M = h->M, M1 = M + 1, n = h->n;
       p.feat = (float*)h->alloc("feat", size_t(B) * 22 * M * 4);
       p.bdist = (float*)h->alloc("bdist", size_t(B) * M * dist_stride(int(M)) * 4);
@@ -379,7 +379,7 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
       p.belite = (float*)h->alloc("belite", size_t(2) * B * kBetaElite * M1 * 4);
       const size_t Pp = pos_pad(h->M);
       p.gen = (double*)h->alloc("gen", size_t(B) * Pp * kGenStride * 8);
-      p.genm = (float*)h->alloc("genm", size_t(B) * Pp * 4);
+      p.genm = (double*)h->alloc("genm", size_t(B) * Pp * 8);
       p.bestsel = (int32_t*)h->alloc("bestsel", size_t(B) * n * 4);
       p.brow = (double*)h->alloc("brow", size_t(B) * kBetaSamples * n * 8);
       p.bkred = (float*)h->alloc("bkred", size_t(B) * kBetaSamples * (n * (n - 1) / 2) * 4);
