@@ -40,7 +40,7 @@ for _p in (ROOT, PKG):
 kF = 22  # beta-CEM features per mother row (cx | cy)
 METRIC = "MPC optimizer steps/s (batch=1024,H=30,obs_samp=500) @1/2/4/8 GPU; % HBM roofline"
 
-# BASELINE.json configs[1] (headline) and configs[2]
+# BASELINE.json configs[1] (headline), configs[2] and configs[3] (per GPU: one configuration per rank)
 WORKLOADS = {
     "mmd_opt": dict(desc="static obs, mmd_opt, batch=1024 rollouts, H=30, num_obs=10, obs_samples=484 (n=22, M=n^2)",
                     cost="mmd_opt", num_reduced=22, num_obs=10, num_prime=30, noise="gaussian", level=0.1,
@@ -48,6 +48,9 @@ WORKLOADS = {
     "cvar": dict(desc="static obs, cvar, batch=1024 rollouts, H=30, num_obs=10, obs_samples=500, beta noise 0.3",
                  cost="cvar", num_reduced=500, num_obs=10, num_prime=30, noise="beta", level=0.3,
                  num_batch=1024),
+    "dynamic": dict(desc="dynamic obs, mmd_opt, batch=1024 rollouts, H=50, num_obs=20, obs_samples=1024 (n=32, M=n^2)",
+                    cost="mmd_opt", num_reduced=32, num_obs=20, num_prime=50, noise="gaussian", level=0.1,
+                    num_batch=1024, variant="dynamic"),
 }
 
 # MI355X peaks (MI355X_MICROARCH.md): fp32 vector 157.3 TFLOP/s = 78.6 T lane-ops/s
@@ -99,6 +102,16 @@ def make_workload(w, rank):
     SURVEY §8d), then idx_mpc = randint(1, 10000) (S/main_mpc.py:114)."""
     from optimizer.cem_helper import Helper  # noqa: F401  (drop-in package import check)
     O = w["num_obs"]
+    init = np.array([0.0, 1.75, 5.0, 0.0, 0.0, 0.0], np.float32)          # S/main_mpc.py:46-54
+    mean = np.array([15] * 4 + [0] * 4, np.float32)                       # S/main_mpc.py:58-71
+    cov = np.diag([20.0] * 4 + [100.0] * 4).astype(np.float32)
+    if w.get("variant") == "dynamic":
+        # synthetic_dynamic_obs/main_mpc.py:34-41,106-129 (ego in the right lane; QP obstacle tracks)
+        from optimizer.obs_data_generate_dynamic import dynamic_obstacles
+        d = dynamic_obstacles(rank, O)
+        init = np.array([0.0, -1.75, 5.0, 0.0, 0.0, 0.0], np.float32)
+        return dict(idx_mpc=d["idx_mpc"], init=init, mean=mean, cov=cov, xo=d["x_traj"], yo=d["y_traj"],
+                    v_des=15.0)
     rs = np.random.RandomState(rank)
     xs = np.arange(35, 35 + 5 * max(9, O), 5, dtype=np.float64)
     x = rs.choice(xs, O, replace=False)
@@ -107,9 +120,6 @@ def make_workload(w, rank):
     # static obstacles: constant position over the 100-point plan (cem_helper.py:366-378 with v = 0)
     xo = np.repeat(x[:, None], 100, axis=1).astype(np.float32)
     yo = np.repeat(y[:, None], 100, axis=1).astype(np.float32)
-    init = np.array([0.0, 1.75, 5.0, 0.0, 0.0, 0.0], np.float32)          # S/main_mpc.py:46-54
-    mean = np.array([15] * 4 + [0] * 4, np.float32)                       # S/main_mpc.py:58-71
-    cov = np.diag([20.0] * 4 + [100.0] * 4).astype(np.float32)
     return dict(idx_mpc=idx_mpc, init=init, mean=mean, cov=cov, xo=xo, yo=yo, v_des=15.0)
 
 
@@ -126,7 +136,7 @@ def cpu_baseline(w, inst, seconds):
         threads = 1
     B = w["num_batch"]
     ora = oracle.CEM(w["num_reduced"], w["num_obs"], w["level"], w["num_prime"], w["noise"], 0.0, 0.0,
-                     num_batch=B, maxiter_cem=1)
+                     num_batch=B, maxiter_cem=1, variant=w.get("variant", "static"))
     draws = oracle.Draws.philox(ora.prob, inst["idx_mpc"], seed=0, with_beta_cem=(w["cost"] == "mmd_opt"))
     st = ora.init_state(inst["init"], inst["mean"], inst["cov"], draws)
     t0 = time.perf_counter()
@@ -183,7 +193,8 @@ def main():
     inst = make_workload(w, rank)
     T = 20
     cfg = _native.make_config(w["num_reduced"], w["num_obs"], w["level"], w["num_prime"], w["noise"], 0.0, 0.0,
-                              num_batch=w["num_batch"], maxiter_cem=T, device=local, seed=rank)
+                              num_batch=w["num_batch"], maxiter_cem=T, device=local, seed=rank,
+                              variant=w.get("variant", "static"))
     h = _native.Handle(cfg)
     stream = torch.cuda.current_stream()
     h.set_stream(stream.cuda_stream)
@@ -254,7 +265,7 @@ def main():
             "metric": METRIC, "value": value, "unit": "steps/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (static obstacle configs k=rank, internal Philox noise)",
+            "data": f"synthetic ({w.get('variant', 'static')} obstacle configs k=rank, internal Philox noise)",
             "config": {"workload": w["desc"], "cost": w["cost"], "global_batch": w["num_batch"] * world,
                        "num_batch": w["num_batch"], "num_prime": w["num_prime"], "num_obs": w["num_obs"],
                        "num_reduced": w["num_reduced"], "noise": w["noise"], "noise_level": w["level"],

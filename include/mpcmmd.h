@@ -185,6 +185,17 @@ int mpcmmd_run_stage(mpcmmd_handle* h, int32_t stage, int32_t t);
  * < 0 on error / when count is too small. */
 int mpcmmd_host_constant(const mpcmmd_config* cfg, const char* name, double* dst, size_t count);
 
+/* Dynamic-obstacle trajectories of the synthetic_dynamic_obs driver:
+ * obs_data.compute_boundary_vec + obs_data.compute_obs_guess
+ * (synthetic_dynamic_obs/obs_data_generate_dynamic.py:56-109, called per
+ * obstacle at synthetic_dynamic_obs/main_mpc.py:116-126).  Obstacle i starts
+ * at (x0[i], y0[i]) with speed (vx0[i], vy0[i]) and zero acceleration and
+ * tracks speed v_des[i] (obs_data.sampling_param, :111-133) and lane y_des
+ * (the driver passes -1.75).  Writes x_traj, y_traj [num_obs][100].  Host
+ * fp64 KKT (inverted once), fp32 output; no GPU needed. */
+int mpcmmd_obs_dynamic_traj(int32_t num_obs, const float* x0, const float* y0, const float* vx0, const float* vy0,
+                            const float* v_des, float y_des, float* x_traj, float* y_traj);
+
 #ifdef __cplusplus
 }
 #endif

@@ -216,4 +216,83 @@ ProblemConsts build_constants(int num_prime, int variant) {
   return c;
 }
 
+DynObsConsts build_dyn_obs_consts() {
+  // obs_data.__init__ (obs_data_generate_dynamic.py:10-36): the same
+  // linspace(0, 15, 100) basis, cast to fp32 by jnp.asarray
+  DynObsConsts c;
+  std::vector<double> P, Pd, Pdd;
+  const auto t = linspace(0.0, 15.0, kNum);
+  bernstein10(t, t.front(), t.back(), P, Pd, Pdd);
+  for (auto* v : {&P, &Pd, &Pdd})
+    for (auto& x : *v) x = round32(x);
+  const double k_p_v = 2.0, k_p = 2.0;
+  std::vector<double> Avd(size_t(kNum) * kNvar), Apd(size_t(kNum) * kNvar);
+  c.colsum_x.assign(kNvar, 0.0);
+  c.colsum_y.assign(kNvar, 0.0);
+  for (int r = 0; r < kNum; ++r)
+    for (int j = 0; j < kNvar; ++j) {
+      const int i = r * kNvar + j;
+      Avd[i] = Pdd[i] - k_p_v * Pd[i];
+      Apd[i] = Pdd[i] - k_p * P[i];
+      c.colsum_x[j] += Avd[i];
+      c.colsum_y[j] += Apd[i];
+    }
+  // cost = 100 Pdd^T Pdd + rho A^T A (:86-90, rho_v = rho_offset = 1)
+  auto sm = atb(Pdd.data(), Pdd.data(), kNum, kNvar, kNvar);
+  auto ax = atb(Avd.data(), Avd.data(), kNum, kNvar, kNvar);
+  auto ay = atb(Apd.data(), Apd.data(), kNum, kNvar, kNvar);
+  std::vector<double> cx(kNvar * kNvar), cy(kNvar * kNvar);
+  for (int i = 0; i < kNvar * kNvar; ++i) {
+    cx[i] = 100.0 * sm[i] + ax[i];
+    cy[i] = 100.0 * sm[i] + ay[i];
+  }
+  // A_eq_x = [P0; Pd0; Pdd0], A_eq_y = [P0; Pd0; Pdd0; Pd_end] (:33-34)
+  std::vector<double> Aeq_x(3 * kNvar), Aeq_y(4 * kNvar);
+  for (int j = 0; j < kNvar; ++j) {
+    Aeq_x[0 * kNvar + j] = Aeq_y[0 * kNvar + j] = P[j];
+    Aeq_x[1 * kNvar + j] = Aeq_y[1 * kNvar + j] = Pd[j];
+    Aeq_x[2 * kNvar + j] = Aeq_y[2 * kNvar + j] = Pdd[j];
+    Aeq_y[3 * kNvar + j] = Pd[(kNum - 1) * kNvar + j];
+  }
+  c.kinv_x = kkt(cx, Aeq_x, 3);
+  c.kinv_y = kkt(cy, Aeq_y, 4);
+  if (!invert(c.kinv_x, 14) || !invert(c.kinv_y, 15)) throw std::runtime_error("singular obstacle KKT");
+  c.P = P;
+  return c;
+}
+
+void dyn_obs_traj(const DynObsConsts& c, int num_obs, const float* x0, const float* y0, const float* vx0,
+                  const float* vy0, const float* v_des, float y_des, float* x_traj, float* y_traj) {
+  // rhs = [-lincost; b_eq] with -lincost = A^T b = -k_p * target * colsum(A)
+  // (:81-96); b_eq_x = [x0, vx0, 0], b_eq_y = [y0, vy0, 0, 0] (:56-71)
+  for (int o = 0; o < num_obs; ++o) {
+    double rx[14], ry[15];
+    const double tv = -2.0 * double(v_des[o]), ty = -2.0 * double(y_des);
+    for (int j = 0; j < kNvar; ++j) {
+      rx[j] = tv * c.colsum_x[j];
+      ry[j] = ty * c.colsum_y[j];
+    }
+    rx[11] = x0[o], rx[12] = vx0[o], rx[13] = 0.0;
+    ry[11] = y0[o], ry[12] = vy0[o], ry[13] = 0.0, ry[14] = 0.0;
+    float cxf[kNvar], cyf[kNvar];
+    for (int j = 0; j < kNvar; ++j) {
+      double sx = 0.0, sy = 0.0;
+      for (int i = 0; i < 14; ++i) sx += c.kinv_x[j * 14 + i] * rx[i];
+      for (int i = 0; i < 15; ++i) sy += c.kinv_y[j * 15 + i] * ry[i];
+      cxf[j] = float(sx);
+      cyf[j] = float(sy);
+    }
+    // x = P c (:104-105), fp32 coefficients, fp64 accumulation
+    for (int r = 0; r < kNum; ++r) {
+      double sx = 0.0, sy = 0.0;
+      for (int j = 0; j < kNvar; ++j) {
+        sx += c.P[r * kNvar + j] * double(cxf[j]);
+        sy += c.P[r * kNvar + j] * double(cyf[j]);
+      }
+      x_traj[size_t(o) * kNum + r] = float(sx);
+      y_traj[size_t(o) * kNum + r] = float(sy);
+    }
+  }
+}
+
 }  // namespace mpcmmd

@@ -39,6 +39,26 @@ struct ProblemConsts {
   std::vector<double> fit;                // [11][H] = (P'^T P' + 0.05 I)^-1 P'^T
 };
 
+// Constant-speed / lane-keeping QP that generates the dynamic obstacles'
+// trajectories: obs_data.compute_obs_guess
+// (synthetic_dynamic_obs/obs_data_generate_dynamic.py:73-109).  One segment
+// over the whole 100-point plan (unlike the 4-segment guess QP of the
+// optimizer), smoothness weight 100, k_p_v = k_p = 2.
+struct DynObsConsts {
+  std::vector<double> P;         // [100][11] fp32-rounded basis
+  std::vector<double> kinv_x;    // [14][14]
+  std::vector<double> kinv_y;    // [15][15]
+  std::vector<double> colsum_x;  // [11] column sums of A_vd = Pdd - k_p_v Pd
+  std::vector<double> colsum_y;  // [11] column sums of A_pd = Pdd - k_p P
+};
+DynObsConsts build_dyn_obs_consts();
+
+// x_traj/y_traj [num_obs][100] fp32 for obstacles starting at (x0, y0) with
+// speeds (vx0, vy0), zero acceleration, tracking speed v_des[i] and lane
+// y_des (dynamic main_mpc.py:116-126 uses y_des = -1.75).
+void dyn_obs_traj(const DynObsConsts& c, int num_obs, const float* x0, const float* y0, const float* vx0,
+                  const float* vy0, const float* v_des, float y_des, float* x_traj, float* y_traj);
+
 // variant: 0 static, 1 dynamic.  Throws std::runtime_error on a singular
 // matrix (never for valid H >= 2).
 ProblemConsts build_constants(int num_prime, int variant);

@@ -722,4 +722,18 @@ int mpcmmd_host_constant(const mpcmmd_config* cfg, const char* name, double* dst
   }
 }
 
+int mpcmmd_obs_dynamic_traj(int32_t num_obs, const float* x0, const float* y0, const float* vx0, const float* vy0,
+                            const float* v_des, float y_des, float* x_traj, float* y_traj) {
+  if (num_obs < 0) return fail(MPCMMD_E_INVALID, "num_obs < 0");
+  if (num_obs > 0 && (!x0 || !y0 || !vx0 || !vy0 || !v_des || !x_traj || !y_traj))
+    return fail(MPCMMD_E_INVALID, "null argument");
+  try {
+    static const DynObsConsts c = build_dyn_obs_consts();
+    dyn_obs_traj(c, num_obs, x0, y0, vx0, vy0, v_des, y_des, x_traj, y_traj);
+    return MPCMMD_OK;
+  } catch (const std::exception& e) {
+    return fail(MPCMMD_E_INVALID, e.what());
+  }
+}
+
 }  // extern "C"

@@ -25,7 +25,7 @@ SYMBOLS = (
     "mpcmmd_destroy", "mpcmmd_set_stream", "mpcmmd_get_stream", "mpcmmd_solve", "mpcmmd_begin",
     "mpcmmd_iterate", "mpcmmd_finish", "mpcmmd_sync", "mpcmmd_profile", "mpcmmd_kernel_times",
     "mpcmmd_kernel_name", "mpcmmd_buffer_info", "mpcmmd_read", "mpcmmd_write", "mpcmmd_run_stage",
-    "mpcmmd_host_constant",
+    "mpcmmd_host_constant", "mpcmmd_obs_dynamic_traj",
 )
 
 
@@ -91,6 +91,7 @@ def lib():
     L.mpcmmd_write.argtypes = [vp, C.c_char_p, vp, C.c_size_t]
     L.mpcmmd_run_stage.argtypes = [vp, C.c_int32, C.c_int32]
     L.mpcmmd_host_constant.argtypes = [C.POINTER(Config), C.c_char_p, C.POINTER(C.c_double), C.c_size_t]
+    L.mpcmmd_obs_dynamic_traj.argtypes = [C.c_int32, fp, fp, fp, fp, fp, C.c_float, fp, fp]
     if L.mpcmmd_abi_version() != ABI_VERSION:
         raise NativeError("libmpcmmd ABI version mismatch")
     _lib = L
@@ -116,6 +117,19 @@ def host_constant(cfg, name):
     out = np.empty(n, np.float64)
     check(L.mpcmmd_host_constant(C.byref(cfg), name.encode(), out.ctypes.data_as(C.POINTER(C.c_double)), n))
     return out
+
+
+def obs_dynamic_traj(x0, y0, vx0, vy0, v_des, y_des=-1.75):
+    """mpcmmd_obs_dynamic_traj: per-obstacle QP trajectories [O][100] x 2
+    (obs_data.compute_obs_guess, obs_data_generate_dynamic.py:73-109)."""
+    a = [np.ascontiguousarray(np.asarray(v, np.float32).reshape(-1)) for v in (x0, y0, vx0, vy0, v_des)]
+    O = a[0].size
+    if any(v.size != O for v in a):
+        raise ValueError("obstacle arrays differ in length")
+    xt = np.empty((O, 100), np.float32)
+    yt = np.empty((O, 100), np.float32)
+    check(lib().mpcmmd_obs_dynamic_traj(O, *[_fptr(v) for v in a], float(y_des), _fptr(xt), _fptr(yt)))
+    return xt, yt
 
 
 def _fptr(a):

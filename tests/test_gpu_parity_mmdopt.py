@@ -48,8 +48,13 @@ def _check_selection(name, got, samples, M, n):
             elite_equal(f"{name}[{s}]", got[s], ref[s], keys[s], tol=1e-6)
 
 
-def _run_mother(native, n, B, H, O, noise, seed):
-    ora, nat, xo, yo = make_pair(native, "mmd_opt", noise, n=n, O=O, H=H, B=B, T=2, acc_c=0.05, steer_c=0.01)
+def _run_mother(native, n, B, H, O, noise, seed, variant="static"):
+    ora, nat, xo, yo = make_pair(native, "mmd_opt", noise, n=n, O=O, H=H, B=B, T=2, acc_c=0.05, steer_c=0.01,
+                                 variant=variant)
+    if variant == "dynamic":   # synthetic_dynamic_obs scenario (obs_data_generate_dynamic.py, library QP)
+        from optimizer.obs_data_generate_dynamic import dynamic_obstacles
+        dyn = dynamic_obstacles(seed, O)
+        xo, yo = dyn["x_traj"], dyn["y_traj"]
     draws = oracle.Draws.random(ora.prob, np.random.default_rng(seed), idx_mpc=11, seed=0, with_beta_cem=True)
     nat.begin("mmd_opt", 11, DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, xo, yo, 15.0, draws)
     st = ora.init_state(DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, draws)
@@ -79,10 +84,12 @@ def test_mother_features(native, noise):
     close("feat_cy", feat[:, 11:].transpose(0, 2, 1), cym, rtol=1e-4, atol=2e-4)
 
 
-@pytest.mark.parametrize("n,B,check", [(5, 20, None), (12, 20, [0, 7, 19]), (22, 20, [0, 19])])
-def test_beta_cem_lockstep(native, n, B, check):
-    H, O = 10, 3
-    ora, nat, xo, yo, draws, st, acc, steer = _run_mother(native, n, B, H, O, "gaussian", 2)
+@pytest.mark.parametrize("n,B,H,O,variant,check", [
+    (5, 20, 10, 3, "static", None), (12, 20, 10, 3, "static", [0, 7, 19]), (22, 20, 10, 3, "static", [0, 19]),
+    # BASELINE configs[3] shape: dynamic obstacles, H = 50, O = 20, n = 32 (M = 1024 mother rollouts)
+    (32, 20, 50, 20, "dynamic", [0, 19])])
+def test_beta_cem_lockstep(native, n, B, H, O, variant, check):
+    ora, nat, xo, yo, draws, st, acc, steer = _run_mother(native, n, B, H, O, "gaussian", 2, variant)
     p = ora.prob
     M = n * n
     M1 = M + 1
