@@ -475,7 +475,7 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
 constexpr int kKerThreads = 1024;
 
 struct KerLds {
-  size_t sel, csg, rowsum, cnt, start, fill, ulist, urank, pairs, pair_s, work, total;
+  size_t sel, csg, cnt, start, fill, ulist, urank, pairs, pair_s, work, total;
   int rows;  // D-chunk rows
 };
 
@@ -489,7 +489,6 @@ HDI KerLds ker_lds(int M, int n, size_t budget) {
   };
   L.sel = take(size_t(kBetaSamples) * n * 2);
   L.csg = take(size_t(kBetaSamples) * 4);
-  L.rowsum = take(size_t(kBetaSamples) * n * 8);
   L.cnt = take(size_t(M) * 4);
   L.start = take(size_t(M) * 4);
   L.fill = take(size_t(M) * 4);
@@ -507,17 +506,21 @@ HDI KerLds ker_lds(int M, int n, size_t budget) {
 }
 
 constexpr size_t kLdsBudget = 160 * 1024 - 1024;
+// k_bkernel runs two workgroups per CU (one's D-row loads overlap the
+// other's exp sums) whenever half the LDS still holds this many D rows
+constexpr size_t kKerHalfBudget = 80 * 1024;
+constexpr int kKerMinRowsHalf = 16;
 constexpr float kNegLog2e = -1.44269504088896340736f;
 
-__global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb) {
+__global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb, int budget) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x, M = p.M, n = p.n, Md = dist_stride(M);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const KerLds C = ker_lds(M, n, kLdsBudget);
+  const KerLds C = ker_lds(M, n, size_t(budget));
   short* sl = reinterpret_cast<short*>(smem + C.sel);
   float* csg = reinterpret_cast<float*>(smem + C.csg);
-  double* rowsum = reinterpret_cast<double*>(smem + C.rowsum);
+  double* rowsum = p.brow + size_t(b) * kBetaSamples * n;
   int* cnt = reinterpret_cast<int*>(smem + C.cnt);
   int* start = reinterpret_cast<int*>(smem + C.start);
   int* fill = reinterpret_cast<int*>(smem + C.fill);
@@ -626,8 +629,6 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb) {
     }
     if (c0 == 0) MPCMMD_STAMP(p, 19);
   }
-  __syncthreads();
-  for (int i = i_lo + tid; i < i_hi; i += kKerThreads) p.brow[size_t(b) * kBetaSamples * n + i] = rowsum[i];
   MPCMMD_STAMP(p, 20);
 }
 
@@ -1186,8 +1187,10 @@ void launch_bqp(const Params& p, int tb, hipStream_t s) {
 }
 
 void launch_bkernel(const Params& p, int tb, hipStream_t s) {
-  const KerLds k = ker_lds(p.M, p.n, kLdsBudget);
-  hipLaunchKernelGGL(k_bkernel, dim3(p.B), dim3(kKerThreads), k.total, s, p, tb);
+  size_t budget = kKerHalfBudget;
+  if (ker_lds(p.M, p.n, budget).rows < kKerMinRowsHalf) budget = kLdsBudget;
+  const KerLds k = ker_lds(p.M, p.n, budget);
+  hipLaunchKernelGGL(k_bkernel, dim3(p.B), dim3(kKerThreads), k.total, s, p, tb, int(budget));
 }
 
 void launch_belite(const Params& p, int tb, hipStream_t s) {
