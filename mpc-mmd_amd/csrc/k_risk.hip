@@ -132,7 +132,31 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
   }
 }
 
+// Beta-noise attempt table of outer iteration t (rng.hpp): one thread per
+// (stream, attempt, r, h)
+__global__ __launch_bounds__(256) void k_gamma_tab(Params p, int t) {
+  const int S = p.S, H = p.H;
+  const int plane = S * H;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= kGammaTabStreams * kGammaTabAttempts * plane) return;
+  const int e = idx % plane, sk = idx / plane;
+  const int k = sk % kGammaTabAttempts, st = sk / kGammaTabAttempts;
+  const int h = e / S, r = e - h * S;
+  const uint32_t k0 = iteration_key0(p.idx_mpc, t), k1 = p.seed;
+  const GammaAttempt g = gamma_attempt(k0, k1, kStreamGammaAccA + uint32_t(st), uint32_t(r) * uint32_t(H) + h, k);
+  double* o = p.gtab + (size_t(sk) * 4) * plane + e;
+  o[0] = g.x;
+  o[plane] = g.u;
+  o[2 * size_t(plane)] = g.lu;
+  o[3 * size_t(plane)] = g.lw;
+}
+
 }  // namespace
+
+void launch_gamma_tab(const Params& p, int t, hipStream_t s) {
+  const int total = kGammaTabStreams * kGammaTabAttempts * p.S * p.H;
+  hipLaunchKernelGGL(k_gamma_tab, dim3((total + 255) / 256), dim3(256), 0, s, p, t);
+}
 
 void launch_risk_baseline(const Params& p, int t, hipStream_t s) {
   const size_t lds = risk_lds_bytes(p.O, p.H, p.S);

@@ -53,10 +53,12 @@ enum KernelId {
   kKBElite,
   kKMmdFinal,
   kKSelect,
+  kKGammaTab,
   kNumKernels
 };
 const char* kKernelNames[kNumKernels] = {"noise",   "front", "risk_baseline", "mother",   "bdist", "bsample",
-                                         "bselect", "bkernel", "bqp",         "belite", "mmdfinal", "select"};
+                                         "bselect", "bkernel", "bqp",         "belite", "mmdfinal", "select",
+                                         "gamma_tab"};
 
 }  // namespace
 
@@ -213,6 +215,7 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
       h->launch(kKFront, [&] { launch_front(p, t, h->stream); });
       break;
     case 2:
+      if (p.noise == MPCMMD_NOISE_BETA) h->launch(kKGammaTab, [&] { launch_gamma_tab(p, t, h->stream); });
       if (p.cost == MPCMMD_COST_MMD_OPT) {
         if (!h->mmd_ok) throw std::invalid_argument("mmd_opt unsupported for this configuration: " + h->mmd_why);
         h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
@@ -233,6 +236,7 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
       if (p.cost != MPCMMD_COST_MMD_OPT || !h->mmd_ok) throw std::invalid_argument("stages 4-8 need cost mmd_opt");
       if (stage >= 5 && stage <= 7 && t >= kBetaIters) throw std::invalid_argument("beta-CEM iteration out of range");
       if (stage == 4) {  // mother rollouts, features and their distance matrix
+        if (p.noise == MPCMMD_NOISE_BETA) h->launch(kKGammaTab, [&] { launch_gamma_tab(p, t, h->stream); });
         h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
         h->launch(kKBDist, [&] { launch_bdist(p, h->stream); });
       }
@@ -365,6 +369,7 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
     p.st0 = (const float*)h->alloc("st0", 8 * 4);
     p.roll = (const float*)h->alloc("roll", size_t(T) * 3 * H * S * 4);
     p.resample = (const float*)h->alloc("resample", size_t(T) * (B - kElite) * 8 * 4);
+    p.gtab = (double*)h->alloc("gtab", c.noise == MPCMMD_NOISE_BETA ? gamma_tab_size(S, H) * 8 : 16);
     if (mmd_ok) {
       p.beta_z0 = (const float*)h->alloc("beta_z0", size_t(kBetaSamples) * (h->M + 1) * 4);
       p.beta_z = (const double*)h->alloc("beta_z", size_t(kBetaIters) * pos_pad(h->M) * kBzCols * 8);

@@ -66,27 +66,75 @@ HDI void philox_normals4(uint32_t k0, uint32_t k1, uint32_t stream, uint32_t wor
   out[3] = r1 * sin(t1);
 }
 
-// Marsaglia-Tsang core (see oracle/rng.py:_log_gamma_parts): returns log G'
-// for alpha' = alpha (+1 when alpha < 1) and the boost log-uniform.
-DEVI void log_gamma_parts(double alpha, uint32_t k0, uint32_t k1, uint32_t stream, uint32_t elem,
-                          double& lg, double& lub) {
+// Marsaglia-Tsang acceptance of attempt (x, u, log u) for d, v3 = (1 + c x)^3:
+// the squeeze u < 1 - 0.0331 x^4 first, the exact log test only when it
+// fails (Marsaglia & Tsang 2000; oracle/rng.py:_log_gamma_parts applies the
+// identical two tests in the identical order).
+HDI bool mt_accept(double x, double u, double lu, double d, double v3) {
+  if (u < 1.0 - 0.0331 * (x * x) * (x * x)) return true;
+  return lu < 0.5 * x * x + d - d * v3 + d * log(v3);
+}
+
+// One Marsaglia-Tsang attempt from the Philox counter (elem, k, stream, 1):
+// words 0,1 -> Box-Muller normal (cos branch), word 2 -> acceptance uniform,
+// word 3 -> boost uniform.
+struct GammaAttempt {
+  double x, u, lu, lw;
+};
+HDI GammaAttempt gamma_attempt(uint32_t k0, uint32_t k1, uint32_t stream, uint32_t elem, int k) {
+  const U4 w = philox4x32_10(U4{elem, uint32_t(k), stream, 1u}, k0, k1);
+  const double two_pi = 6.283185307179586;
+  const double r = sqrt(-2.0 * log(u01(w.x)));
+  GammaAttempt a;
+  a.x = r * cos(two_pi * u01(w.y));
+  a.u = u01(w.z);
+  a.lu = log(a.u);
+  a.lw = log(u01(w.w));
+  return a;
+}
+
+// Attempt table of one outer iteration: the Philox-derived (x, u, log u,
+// log w) of attempts 0..kGammaTabAttempts-1 for every (stream, row r, step h).
+// The uniforms of the Beta noise depend only on (key, stream, r, h) -- the
+// same realisation for every candidate (cem_helper.py:110, Q2) -- so they
+// are drawn once per iteration instead of once per candidate; each
+// candidate applies only its own (alpha-dependent) transform.  Layout
+// [stream 0..3][k][field 0..3][h][r] (r fastest: coalesced per sample row).
+constexpr int kGammaTabAttempts = 4;
+constexpr int kGammaTabStreams = 4;  // acc A, acc B, steer A, steer B
+HDI size_t gamma_tab_size(int S, int H) { return size_t(kGammaTabStreams) * kGammaTabAttempts * 4 * S * H; }
+
+// log G' for alpha' = alpha (+1 when alpha < 1) and the boost log-uniform,
+// from the table (attempts < kGammaTabAttempts) then Philox directly.
+DEVI void log_gamma_parts_tab(double alpha, const double* tab, int S, int H, int r, int h, uint32_t k0,
+                              uint32_t k1, uint32_t stream, uint32_t elem, double& lg, double& lub) {
   const double a1 = alpha < 1.0 ? alpha + 1.0 : alpha;
   const double d = a1 - 1.0 / 3.0;
   const double c = 1.0 / sqrt(9.0 * d);
-  const double two_pi = 6.283185307179586;
+  const size_t plane = size_t(S) * H, at = size_t(h) * S + r;
   lg = log(d);
   lub = 0.0;
-  for (int k = 0; k < kGammaMaxAttempts; ++k) {
-    const U4 u = philox4x32_10(U4{elem, uint32_t(k), stream, 1u}, k0, k1);
-    const double r = sqrt(-2.0 * log(u01(u.x)));
-    const double x = r * cos(two_pi * u01(u.y));
+  for (int k = 0; k < kGammaTabAttempts; ++k) {
+    const double* t = tab + size_t(k) * 4 * plane + at;
+    const double x = t[0];
     const double v = 1.0 + c * x;
     if (v > 0.0) {
       const double v3 = v * v * v;
-      const double lu = log(u01(u.z));
-      if (lu < 0.5 * x * x + d - d * v3 + d * log(v3)) {
+      if (mt_accept(x, t[plane], t[2 * plane], d, v3)) {
         lg = log(d * v3);
-        lub = log(u01(u.w));
+        lub = t[3 * plane];
+        return;
+      }
+    }
+  }
+  for (int k = kGammaTabAttempts; k < kGammaMaxAttempts; ++k) {
+    const GammaAttempt g = gamma_attempt(k0, k1, stream, elem, k);
+    const double v = 1.0 + c * g.x;
+    if (v > 0.0) {
+      const double v3 = v * v * v;
+      if (mt_accept(g.x, g.u, g.lu, d, v3)) {
+        lg = log(d * v3);
+        lub = g.lw;
         return;
       }
     }
@@ -94,12 +142,15 @@ DEVI void log_gamma_parts(double alpha, uint32_t k0, uint32_t k1, uint32_t strea
 }
 
 // Beta(a, b) with a = ra*s, b = rb*s (s = |control|); s == 0 takes the
-// alpha -> 0+ limit (oracle/rng.py:beta_draws, DESIGN.md Numerics).
-DEVI float beta_draw(double a, double b, double ra, double rb, uint32_t k0, uint32_t k1, uint32_t stream_a,
-                     uint32_t stream_b, uint32_t elem) {
+// alpha -> 0+ limit (oracle/rng.py:beta_draws, DESIGN.md Numerics).  tab_a,
+// tab_b: the attempt-table slices of the two gamma streams.
+DEVI float beta_draw_tab(double a, double b, double ra, double rb, const double* tab_a, const double* tab_b,
+                         int S, int H, int r, int h, uint32_t k0, uint32_t k1, uint32_t stream_a,
+                         uint32_t stream_b) {
+  const uint32_t elem = uint32_t(r) * uint32_t(H) + uint32_t(h);
   double ga, ua, gb, ub;
-  log_gamma_parts(a, k0, k1, stream_a, elem, ga, ua);
-  log_gamma_parts(b, k0, k1, stream_b, elem, gb, ub);
+  log_gamma_parts_tab(a, tab_a, S, H, r, h, k0, k1, stream_a, elem, ga, ua);
+  log_gamma_parts_tab(b, tab_b, S, H, r, h, k0, k1, stream_b, elem, gb, ub);
   if (a == 0.0 && b == 0.0) return (ua * rb > ub * ra) ? 1.0f : 0.0f;
   const double la = a < 1.0 ? ga + ua / a : ga;
   const double lb = b < 1.0 ? gb + ub / b : gb;

@@ -12,7 +12,8 @@ constexpr float kWheelBase = 2.5f;   // cem.py:26
 // Noisy controls of noise row r at step h of outer iteration t
 // (cem_helper.py:405-443 baseline / 469-508 opt; one realisation shared by
 // every candidate, Q2).  Gaussian rows come from p.roll [T][3][H][S]; Beta
-// draws from the Philox gamma streams (elements r*H + h).
+// draws from the Philox gamma streams (elements r*H + h) through the
+// iteration's attempt table p.gtab (k_gamma_tab).
 DEVI void noisy_control(const Params& p, int t, int r, int h, float a, float s, float& an, float& sn) {
   const int S = p.S, H = p.H;
   const float* roll = p.roll + size_t(t) * 3 * H * S;
@@ -23,12 +24,12 @@ DEVI void noisy_control(const Params& p, int t, int r, int h, float a, float s, 
     sp = (p.sigma_steer * fabsf(s)) * roll[(1 * H + h) * S + r];
   } else {
     const uint32_t k0 = iteration_key0(p.idx_mpc, t), k1 = p.seed;
-    const uint32_t elem = uint32_t(r) * uint32_t(H) + uint32_t(h);
+    const size_t sl = size_t(kGammaTabAttempts) * 4 * S * H;  // one stream's table
     const float fa = fabsf(a), fs = fabsf(s);
-    const float nba = beta_draw(double(2.0f * fa), double(5.0f * fa), 2.0, 5.0, k0, k1, kStreamGammaAccA,
-                                kStreamGammaAccB, elem);
-    const float nbs = beta_draw(double(2.0f * fs), double(5.0f * fs), 2.0, 5.0, k0, k1, kStreamGammaSteerA,
-                                kStreamGammaSteerB, elem);
+    const float nba = beta_draw_tab(double(2.0f * fa), double(5.0f * fa), 2.0, 5.0, p.gtab, p.gtab + sl, S, H, r, h,
+                                    k0, k1, kStreamGammaAccA, kStreamGammaAccB);
+    const float nbs = beta_draw_tab(double(2.0f * fs), double(5.0f * fs), 2.0, 5.0, p.gtab + 2 * sl,
+                                    p.gtab + 3 * sl, S, H, r, h, k0, k1, kStreamGammaSteerA, kStreamGammaSteerB);
     ap = p.sigma_acc * (2.0f * nba - 1.0f);
     sp = p.K_steer * (2.0f * nbs - 1.0f);  // K_steer holds float32(K_steer * sigma_steer)
   }

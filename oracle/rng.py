@@ -97,7 +97,10 @@ def _log_gamma_parts(alpha, key, stream, elem):
     alpha < 1 (boost), in fp64.  Returns (log G', log U_boost).
 
     Attempt k uses counter (elem, k, stream, 1): words 0,1 -> Box-Muller normal
-    (cos branch), word 2 -> acceptance uniform, word 3 -> boost uniform.
+    (cos branch), word 2 -> acceptance uniform (squeeze, then log test), word
+    3 -> boost uniform.  The GPU reads attempts 0..3 from a per-iteration
+    table of these same values (csrc/rng.hpp: k_gamma_tab); that is caching,
+    not a different stream.
     Not accepted after GAMMA_MAX_ATTEMPTS -> G' = d (never observed).
     """
     alpha = np.asarray(alpha, dtype=np.float64)
@@ -115,8 +118,12 @@ def _log_gamma_parts(alpha, key, stream, elem):
         v = 1.0 + c * x
         vpos = v > 0.0
         v3 = np.where(vpos, v * v * v, 1.0)
-        lu = np.log(_u01(u[2]))
-        acc = vpos & (lu < 0.5 * x * x + d - d * v3 + d * np.log(v3))
+        uu = _u01(u[2])
+        lu = np.log(uu)
+        # squeeze first, exact log test when it fails (Marsaglia & Tsang 2000;
+        # csrc/rng.hpp: mt_accept evaluates the same two tests)
+        squeeze = uu < 1.0 - 0.0331 * (x * x) * (x * x)
+        acc = vpos & (squeeze | (lu < 0.5 * x * x + d - d * v3 + d * np.log(v3)))
         newly = acc & ~done
         out = np.where(newly, np.log(d * v3), out)
         logub = np.where(newly, np.log(_u01(u[3])), logub)
