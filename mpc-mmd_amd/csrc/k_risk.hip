@@ -84,6 +84,7 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
     L.st[h] = p.steer[size_t(b) * 100 + h];
   }
   __syncthreads();
+  const float* bpl = p.noise == 1 ? p.bplane + size_t(b) * 2 * H * S : nullptr;
   for (int r = threadIdx.x; r < S; r += blockDim.x) {
     float x = p.st0[0], y = p.st0[1], vx = p.st0[2], vy = p.st0[3], psi = p.st0[4];
     float cb = 0.0f, lb = 0.0f, ub = 0.0f;
@@ -101,7 +102,7 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
       ub = fmaxf(ub, u1);
       if (h == H - 1) break;  // the last step's state is never recorded
       float an, sn;
-      noisy_control(p, t, r, h, L.a[h], L.st[h], an, sn);
+      noisy_control<true>(p, t, r, h, L.a[h], L.st[h], an, sn, bpl);
       bicycle_step(x, y, vx, vy, psi, an, sn);
     }
     const float qnan = __int_as_float(0x7fc00000);
@@ -151,7 +152,26 @@ __global__ __launch_bounds__(256) void k_gamma_tab(Params p, int t) {
   o[3 * size_t(plane)] = g.lw;
 }
 
+// Beta draws of every (candidate, row, step) of the baseline rollouts:
+// thread (r) of block (h, b); written [B][2][H][S] for k_risk_baseline, so
+// the rollout kernel stays fp32 and its occupancy is not set by the fp64
+// gamma sampler
+__global__ __launch_bounds__(256) void k_beta_planes(Params p, int t) {
+  const int S = p.S, H = p.H;
+  const int r = blockIdx.x * blockDim.x + threadIdx.x, h = blockIdx.y, b = blockIdx.z;
+  if (r >= S) return;
+  float nba, nbs;
+  beta_pair(p, t, r, h, p.acc[size_t(b) * 100 + h], p.steer[size_t(b) * 100 + h], nba, nbs);
+  float* o = p.bplane + size_t(b) * 2 * H * S;
+  o[size_t(h) * S + r] = nba;
+  o[(size_t(H) + h) * S + r] = nbs;
+}
+
 }  // namespace
+
+void launch_beta_planes(const Params& p, int t, hipStream_t s) {
+  hipLaunchKernelGGL(k_beta_planes, dim3((p.S + 255) / 256, p.H, p.B), dim3(256), 0, s, p, t);
+}
 
 void launch_gamma_tab(const Params& p, int t, hipStream_t s) {
   const int total = kGammaTabStreams * kGammaTabAttempts * p.S * p.H;

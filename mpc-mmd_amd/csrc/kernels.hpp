@@ -54,6 +54,7 @@ struct Params {
   // noise tables, device layout (iteration-major, sample-minor for coalescing)
   const float* roll;       // [T][3][H][S]
   const float* resample;   // [T][B-5][8]
+  float* bplane;           // [B][2][H][S] Beta draws (acc, steer) of the baseline rollouts (beta noise)
   double* gtab;            // Beta-noise attempt table of the current iteration (rng.hpp: gamma_tab_size)
   const float* beta_z0;    // [100][M+1]
   const double* beta_z;    // [20][pos_pad(M)][kBzCols] fp32 normals held as fp64 (position-major, zero padded)
@@ -109,6 +110,7 @@ void launch_front(const Params& p, int t, hipStream_t s);
 void launch_select(const Params& p, int t, hipStream_t s);
 void launch_risk_baseline(const Params& p, int t, hipStream_t s);
 void launch_gamma_tab(const Params& p, int t, hipStream_t s);
+void launch_beta_planes(const Params& p, int t, hipStream_t s);
 // mmd_opt risk, one launch each (mpcmmd.hip chains them)
 void launch_mother(const Params& p, int t, hipStream_t s);
 void launch_bdist(const Params& p, hipStream_t s);

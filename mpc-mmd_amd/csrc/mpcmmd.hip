@@ -54,11 +54,12 @@ enum KernelId {
   kKMmdFinal,
   kKSelect,
   kKGammaTab,
+  kKBetaPlanes,
   kNumKernels
 };
 const char* kKernelNames[kNumKernels] = {"noise",   "front", "risk_baseline", "mother",   "bdist", "bsample",
                                          "bselect", "bkernel", "bqp",         "belite", "mmdfinal", "select",
-                                         "gamma_tab"};
+                                         "gamma_tab", "beta_planes"};
 
 }  // namespace
 
@@ -222,8 +223,10 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
         h->launch(kKBDist, [&] { launch_bdist(p, h->stream); });
         for (int tb = 0; tb < kBetaIters; ++tb) run_beta_iteration(h, tb);
         h->launch(kKMmdFinal, [&] { launch_mmdfinal(p, t, h->stream); });
-      } else
+      } else {
+        if (p.noise == MPCMMD_NOISE_BETA) h->launch(kKBetaPlanes, [&] { launch_beta_planes(p, t, h->stream); });
         h->launch(kKRiskBaseline, [&] { launch_risk_baseline(p, t, h->stream); });
+      }
       break;
     case 3:
       h->launch(kKSelect, [&] { launch_select(p, t, h->stream); });
@@ -369,6 +372,7 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
     p.st0 = (const float*)h->alloc("st0", 8 * 4);
     p.roll = (const float*)h->alloc("roll", size_t(T) * 3 * H * S * 4);
     p.resample = (const float*)h->alloc("resample", size_t(T) * (B - kElite) * 8 * 4);
+    p.bplane = (float*)h->alloc("bplane", c.noise == MPCMMD_NOISE_BETA ? size_t(B) * 2 * H * S * 4 : 16);
     p.gtab = (double*)h->alloc("gtab", c.noise == MPCMMD_NOISE_BETA ? gamma_tab_size(S, H) * 8 : 16);
     if (mmd_ok) {
       p.beta_z0 = (const float*)h->alloc("beta_z0", size_t(kBetaSamples) * (h->M + 1) * 4);

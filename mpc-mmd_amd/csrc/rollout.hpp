@@ -9,12 +9,28 @@ namespace mpcmmd {
 constexpr float kDt = 0.15f;         // cem.py:40
 constexpr float kWheelBase = 2.5f;   // cem.py:26
 
+// The two Beta draws of (candidate controls a, s; row r, step h)
+// (cem_helper.py:427-433): Beta(2|a|, 5|a|), Beta(2|s|, 5|s|).
+DEVI void beta_pair(const Params& p, int t, int r, int h, float a, float s, float& nba, float& nbs) {
+  const int S = p.S, H = p.H;
+  const uint32_t k0 = iteration_key0(p.idx_mpc, t), k1 = p.seed;
+  const size_t sl = size_t(kGammaTabAttempts) * 4 * S * H;  // one stream's table
+  const float fa = fabsf(a), fs = fabsf(s);
+  nba = beta_draw_tab(double(2.0f * fa), double(5.0f * fa), 2.0, 5.0, p.gtab, p.gtab + sl, S, H, r, h, k0, k1,
+                      kStreamGammaAccA, kStreamGammaAccB);
+  nbs = beta_draw_tab(double(2.0f * fs), double(5.0f * fs), 2.0, 5.0, p.gtab + 2 * sl, p.gtab + 3 * sl, S, H, r, h,
+                      k0, k1, kStreamGammaSteerA, kStreamGammaSteerB);
+}
+
 // Noisy controls of noise row r at step h of outer iteration t
 // (cem_helper.py:405-443 baseline / 469-508 opt; one realisation shared by
 // every candidate, Q2).  Gaussian rows come from p.roll [T][3][H][S]; Beta
 // draws from the Philox gamma streams (elements r*H + h) through the
 // iteration's attempt table p.gtab (k_gamma_tab).
-DEVI void noisy_control(const Params& p, int t, int r, int h, float a, float s, float& an, float& sn) {
+// kPlanes: Beta draws read from bpl (k_beta_planes) instead of sampled here.
+template <bool kPlanes = false>
+DEVI void noisy_control(const Params& p, int t, int r, int h, float a, float s, float& an, float& sn,
+                        const float* bpl = nullptr) {
   const int S = p.S, H = p.H;
   const float* roll = p.roll + size_t(t) * 3 * H * S;
   const float nc = roll[(2 * H + h) * S + r];
@@ -23,13 +39,13 @@ DEVI void noisy_control(const Params& p, int t, int r, int h, float a, float s, 
     ap = (p.sigma_acc * fabsf(a)) * roll[(0 * H + h) * S + r];
     sp = (p.sigma_steer * fabsf(s)) * roll[(1 * H + h) * S + r];
   } else {
-    const uint32_t k0 = iteration_key0(p.idx_mpc, t), k1 = p.seed;
-    const size_t sl = size_t(kGammaTabAttempts) * 4 * S * H;  // one stream's table
-    const float fa = fabsf(a), fs = fabsf(s);
-    const float nba = beta_draw_tab(double(2.0f * fa), double(5.0f * fa), 2.0, 5.0, p.gtab, p.gtab + sl, S, H, r, h,
-                                    k0, k1, kStreamGammaAccA, kStreamGammaAccB);
-    const float nbs = beta_draw_tab(double(2.0f * fs), double(5.0f * fs), 2.0, 5.0, p.gtab + 2 * sl,
-                                    p.gtab + 3 * sl, S, H, r, h, k0, k1, kStreamGammaSteerA, kStreamGammaSteerB);
+    float nba, nbs;
+    if constexpr (kPlanes) {  // precomputed by k_beta_planes: [2][H][S] of this candidate
+      nba = bpl[size_t(h) * S + r];
+      nbs = bpl[(size_t(H) + h) * S + r];
+    } else {
+      beta_pair(p, t, r, h, a, s, nba, nbs);
+    }
     ap = p.sigma_acc * (2.0f * nba - 1.0f);
     sp = p.K_steer * (2.0f * nbs - 1.0f);  // K_steer holds float32(K_steer * sigma_steer)
   }
