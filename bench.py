@@ -56,6 +56,7 @@ WORKLOADS = {
 # MI355X peaks (MI355X_MICROARCH.md): fp32 vector 157.3 TFLOP/s = 78.6 T lane-ops/s
 # (one fp32 op per lane per cycle at full packing); HBM3E 8 TB/s
 VALU_PEAK_TOPS = 78.6
+VALU64_PEAK_TOPS = 39.3   # fp64 vector 78.6 TFLOP/s = 39.3 T lane-ops/s
 HBM_PEAK_GBS = 8000.0
 
 
@@ -78,6 +79,10 @@ def kernel_work(w, name, launches, stats):
         return "ops", stats[1] * (M + (n - 1) / 2) * 3
     if name == "bdist":
         return "ops", launches * B * M * M * kF * 2
+    if name == "beta_planes":
+        # B x S x H x 2 Beta draws; per draw 2 gammas x (table transform 9 + log 1 + squeeze 5) + la/lb 4
+        # + exp 1 + ratio 2 = 37 fp64 lane-ops (a transcendental / divide / sqrt counted as 1)
+        return "ops64", launches * B * n * H * 2 * 37
     if name == "risk_baseline":
         beta = 2 * 160 if w["noise"] == "beta" else 0
         return "ops", launches * B * n * H * (40 + O * 9 + beta)
@@ -254,10 +259,13 @@ def main():
         launches, tot_ms = busy[dom]
         avg_s = tot_ms / launches / 1e3
         model = kernel_work(w, dom, launches, stats)
-        roof = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_TOPS, "unit": "Tops/s", "frac": None}
+        peak = VALU64_PEAK_TOPS if model is not None and model[0] == "ops64" else VALU_PEAK_TOPS
+        roof = {"bound": "valu", "achieved": None, "peak": peak, "unit": "Tops/s", "frac": None}
         if model is not None:
             roof["achieved"] = model[1] / launches / avg_s / 1e12
-            roof["frac"] = roof["achieved"] / VALU_PEAK_TOPS
+            roof["frac"] = roof["achieved"] / peak
+            if model[0] == "ops64":
+                roof["bound"] = "valu-fp64"
         roof["traffic"] = pmc_traffic(dom)
         roof["kernel"] = dom
         roof["avg_us"] = avg_s * 1e6

@@ -159,9 +159,16 @@ __global__ __launch_bounds__(256) void k_gamma_tab(Params p, int t) {
 __global__ __launch_bounds__(256) void k_beta_planes(Params p, int t) {
   const int S = p.S, H = p.H;
   const int r = blockIdx.x * blockDim.x + threadIdx.x, h = blockIdx.y, b = blockIdx.z;
+  __shared__ MtConst mc[4];
+  const float a = p.acc[size_t(b) * 100 + h], st = p.steer[size_t(b) * 100 + h];
+  if (threadIdx.x < 4) {  // alphas 2|a|, 5|a|, 2|s|, 5|s| of this (candidate, step)
+    const float f = threadIdx.x < 2 ? fabsf(a) : fabsf(st);
+    mc[threadIdx.x] = mt_const(double((threadIdx.x & 1 ? 5.0f : 2.0f) * f));
+  }
+  __syncthreads();
   if (r >= S) return;
   float nba, nbs;
-  beta_pair(p, t, r, h, p.acc[size_t(b) * 100 + h], p.steer[size_t(b) * 100 + h], nba, nbs);
+  beta_pair(p, t, r, h, a, st, nba, nbs, mc);
   float* o = p.bplane + size_t(b) * 2 * H * S;
   o[size_t(h) * S + r] = nba;
   o[(size_t(H) + h) * S + r] = nbs;

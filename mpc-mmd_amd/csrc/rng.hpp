@@ -106,11 +106,17 @@ HDI size_t gamma_tab_size(int S, int H) { return size_t(kGammaTabStreams) * kGam
 
 // log G' for alpha' = alpha (+1 when alpha < 1) and the boost log-uniform,
 // from the table (attempts < kGammaTabAttempts) then Philox directly.
-DEVI void log_gamma_parts_tab(double alpha, const double* tab, int S, int H, int r, int h, uint32_t k0,
-                              uint32_t k1, uint32_t stream, uint32_t elem, double& lg, double& lub) {
+struct MtConst {
+  double d, c;
+};
+HDI MtConst mt_const(double alpha) {
   const double a1 = alpha < 1.0 ? alpha + 1.0 : alpha;
   const double d = a1 - 1.0 / 3.0;
-  const double c = 1.0 / sqrt(9.0 * d);
+  return MtConst{d, 1.0 / sqrt(9.0 * d)};
+}
+DEVI void log_gamma_parts_tab(MtConst mc, const double* tab, int S, int H, int r, int h, uint32_t k0, uint32_t k1,
+                              uint32_t stream, uint32_t elem, double& lg, double& lub) {
+  const double d = mc.d, c = mc.c;
   const size_t plane = size_t(S) * H, at = size_t(h) * S + r;
   lg = log(d);
   lub = 0.0;
@@ -144,19 +150,24 @@ DEVI void log_gamma_parts_tab(double alpha, const double* tab, int S, int H, int
 // Beta(a, b) with a = ra*s, b = rb*s (s = |control|); s == 0 takes the
 // alpha -> 0+ limit (oracle/rng.py:beta_draws, DESIGN.md Numerics).  tab_a,
 // tab_b: the attempt-table slices of the two gamma streams.
-DEVI float beta_draw_tab(double a, double b, double ra, double rb, const double* tab_a, const double* tab_b,
-                         int S, int H, int r, int h, uint32_t k0, uint32_t k1, uint32_t stream_a,
-                         uint32_t stream_b) {
+// mc_a, mc_b: mt_const(a), mt_const(b) (shared by every row r of a step).
+DEVI float beta_draw_tab(double a, double b, double ra, double rb, MtConst mc_a, MtConst mc_b,
+                         const double* tab_a, const double* tab_b, int S, int H, int r, int h, uint32_t k0,
+                         uint32_t k1, uint32_t stream_a, uint32_t stream_b) {
   const uint32_t elem = uint32_t(r) * uint32_t(H) + uint32_t(h);
   double ga, ua, gb, ub;
-  log_gamma_parts_tab(a, tab_a, S, H, r, h, k0, k1, stream_a, elem, ga, ua);
-  log_gamma_parts_tab(b, tab_b, S, H, r, h, k0, k1, stream_b, elem, gb, ub);
+  log_gamma_parts_tab(mc_a, tab_a, S, H, r, h, k0, k1, stream_a, elem, ga, ua);
+  log_gamma_parts_tab(mc_b, tab_b, S, H, r, h, k0, k1, stream_b, elem, gb, ub);
   if (a == 0.0 && b == 0.0) return (ua * rb > ub * ra) ? 1.0f : 0.0f;
   const double la = a < 1.0 ? ga + ua / a : ga;
   const double lb = b < 1.0 ? gb + ub / b : gb;
-  const double lm = la > lb ? la : lb;
-  const double ea = exp(la - lm), eb = exp(lb - lm);
-  return float(ea / (ea + eb));
+  // exp(la - lm), exp(lb - lm) with lm = max(la, lb): one of them is exp(0) = 1 exactly
+  if (la > lb) {
+    const double eb = exp(lb - la);
+    return float(1.0 / (1.0 + eb));
+  }
+  const double ea = exp(la - lb);
+  return float(ea / (ea + 1.0));
 }
 
 }  // namespace mpcmmd

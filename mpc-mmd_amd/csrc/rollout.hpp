@@ -10,16 +10,26 @@ constexpr float kDt = 0.15f;         // cem.py:40
 constexpr float kWheelBase = 2.5f;   // cem.py:26
 
 // The two Beta draws of (candidate controls a, s; row r, step h)
-// (cem_helper.py:427-433): Beta(2|a|, 5|a|), Beta(2|s|, 5|s|).
-DEVI void beta_pair(const Params& p, int t, int r, int h, float a, float s, float& nba, float& nbs) {
+// (cem_helper.py:427-433): Beta(2|a|, 5|a|), Beta(2|s|, 5|s|).  mc: the four
+// Marsaglia-Tsang constants of (2|a|, 5|a|, 2|s|, 5|s|) when the caller
+// shares them across rows (else computed here).
+DEVI void beta_pair(const Params& p, int t, int r, int h, float a, float s, float& nba, float& nbs,
+                    const MtConst* mc = nullptr) {
   const int S = p.S, H = p.H;
   const uint32_t k0 = iteration_key0(p.idx_mpc, t), k1 = p.seed;
   const size_t sl = size_t(kGammaTabAttempts) * 4 * S * H;  // one stream's table
   const float fa = fabsf(a), fs = fabsf(s);
-  nba = beta_draw_tab(double(2.0f * fa), double(5.0f * fa), 2.0, 5.0, p.gtab, p.gtab + sl, S, H, r, h, k0, k1,
-                      kStreamGammaAccA, kStreamGammaAccB);
-  nbs = beta_draw_tab(double(2.0f * fs), double(5.0f * fs), 2.0, 5.0, p.gtab + 2 * sl, p.gtab + 3 * sl, S, H, r, h,
-                      k0, k1, kStreamGammaSteerA, kStreamGammaSteerB);
+  const double aa = double(2.0f * fa), ab = double(5.0f * fa), sa = double(2.0f * fs), sb = double(5.0f * fs);
+  MtConst m[4];
+  if (mc) {
+    for (int i = 0; i < 4; ++i) m[i] = mc[i];
+  } else {
+    m[0] = mt_const(aa), m[1] = mt_const(ab), m[2] = mt_const(sa), m[3] = mt_const(sb);
+  }
+  nba = beta_draw_tab(aa, ab, 2.0, 5.0, m[0], m[1], p.gtab, p.gtab + sl, S, H, r, h, k0, k1, kStreamGammaAccA,
+                      kStreamGammaAccB);
+  nbs = beta_draw_tab(sa, sb, 2.0, 5.0, m[2], m[3], p.gtab + 2 * sl, p.gtab + 3 * sl, S, H, r, h, k0, k1,
+                      kStreamGammaSteerA, kStreamGammaSteerB);
 }
 
 // Noisy controls of noise row r at step h of outer iteration t
