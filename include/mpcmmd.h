@@ -196,6 +196,38 @@ int mpcmmd_host_constant(const mpcmmd_config* cfg, const char* name, double* dst
 int mpcmmd_obs_dynamic_traj(int32_t num_obs, const float* x0, const float* y0, const float* vx0, const float* vy0,
                             const float* v_des, float y_des, float* x_traj, float* y_traj);
 
+/* Monte-Carlo validation of saved optima on the GPU: synthetic_static_obs/
+ * validation.py compute_stats (:134-171) for num_cfg configurations at
+ * once.  Per configuration k: controls of the saved trajectory (cx, cy)
+ * (compute_controls :122-132), num_rollouts noisy fp64 rollouts from
+ * init_state (compute_rollout_complete :42-101), then
+ *   count[k]      = max over (obstacle, step) of #rollouts inside the ellipse
+ *   count_lane[k] = max_step #(y < y_lb) + max_step #(y > y_ub)
+ * (:153-169).  x_obs / y_obs: [num_cfg][num_obs][100] obstacle tracks
+ * (compute_obs_trajectories).  draws: [num_cfg][3][num_rollouts][num_prime]
+ * fp64 -- gaussian: the standard normals of acc, steer, const noise; beta:
+ * the Beta(2|acc|, 5|acc|) and Beta(2|steer|+1e-5, 5|steer|+1e-5) draws and
+ * the const normals -- or NULL for the library's Philox streams keyed by
+ * (keys[k], seed).  Synchronous; allocates its own device buffers. */
+typedef struct mpcmmd_validate_args {
+  int32_t num_cfg, num_obs, num_prime, num_rollouts;
+  int32_t noise;          /* MPCMMD_NOISE_* */
+  int32_t variant;        /* MPCMMD_VARIANT_* (y_lb, y_ub, K_steer) */
+  double noise_level, acc_const_noise, steer_const_noise;
+  uint32_t seed;
+  int32_t device;
+  const double* cx;       /* [num_cfg][11] */
+  const double* cy;
+  const double* init_state; /* [num_cfg][6] */
+  const float* x_obs;
+  const float* y_obs;
+  const double* draws;
+  const uint32_t* keys;   /* [num_cfg] (validation.py seeds np.random with the config key) */
+  int32_t* count;         /* [num_cfg] out */
+  int32_t* count_lane;    /* [num_cfg] out */
+} mpcmmd_validate_args;
+int mpcmmd_validate(const mpcmmd_validate_args* args);
+
 #ifdef __cplusplus
 }
 #endif

@@ -109,6 +109,26 @@ void launch_noise(const Params& p, int t, hipStream_t s);
 void launch_front(const Params& p, int t, hipStream_t s);
 void launch_select(const Params& p, int t, hipStream_t s);
 void launch_risk_baseline(const Params& p, int t, hipStream_t s);
+
+// Monte-Carlo validation (k_validate.hip; S/validation.py:134-171)
+struct ValidateParams {
+  int32_t K, O, H, R, noise;
+  double noise_level, acc_const, steer_const, K_steer, y_lb, y_ub;
+  uint32_t seed;
+  const float* Pdot;    // [100][11] fp32 basis
+  const float* Pddot;
+  const double* cx;     // [K][11]
+  const double* cy;
+  const double* init_state;  // [K][6]
+  const float* x_obs;   // [K][O][100]
+  const float* y_obs;
+  const double* draws;  // [K][3][R][H] or null (internal Philox)
+  const uint32_t* keys; // [K]
+  int32_t* count;       // [K]
+  int32_t* count_lane;  // [K]
+};
+bool validate_shape_ok(int O, int H);
+void launch_validate(const ValidateParams& v, hipStream_t s);
 void launch_gamma_tab(const Params& p, int t, hipStream_t s);
 void launch_beta_planes(const Params& p, int t, hipStream_t s);
 // mmd_opt risk, one launch each (mpcmmd.hip chains them)

@@ -731,6 +731,63 @@ int mpcmmd_host_constant(const mpcmmd_config* cfg, const char* name, double* dst
   }
 }
 
+int mpcmmd_validate(const mpcmmd_validate_args* a) {
+  if (!a) return fail(MPCMMD_E_INVALID, "null argument");
+  const int K = a->num_cfg, O = a->num_obs, H = a->num_prime, R = a->num_rollouts;
+  if (K < 0 || R < 1 || !validate_shape_ok(O, H)) return fail(MPCMMD_E_INVALID, "validate: shape out of range");
+  if (a->noise != MPCMMD_NOISE_GAUSSIAN && a->noise != MPCMMD_NOISE_BETA) return fail(MPCMMD_E_INVALID, "noise");
+  if (K == 0) return MPCMMD_OK;
+  if (!a->cx || !a->cy || !a->init_state || !a->x_obs || !a->y_obs || !a->keys || !a->count || !a->count_lane)
+    return fail(MPCMMD_E_INVALID, "null argument");
+  return guarded([&] {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) throw HipError("no HIP device visible");
+    if (a->device < 0 || a->device >= ndev) throw std::invalid_argument("device out of range");
+    HIPC(hipSetDevice(a->device));
+    const ProblemConsts pc = build_constants(H, a->variant);
+    std::vector<float> basis(2 * kNum * kNvar);
+    for (int i = 0; i < kNum * kNvar; ++i) {
+      basis[i] = float(pc.Pd[i]);
+      basis[kNum * kNvar + i] = float(pc.Pdd[i]);
+    }
+    std::vector<std::pair<void*, size_t>> bufs;
+    auto up = [&](const void* src, size_t bytes) -> void* {
+      void* d = nullptr;
+      HIPC(hipMalloc(&d, bytes));
+      bufs.push_back({d, bytes});
+      if (src) HIPC(hipMemcpy(d, src, bytes, hipMemcpyHostToDevice));
+      return d;
+    };
+    struct Free {
+      std::vector<std::pair<void*, size_t>>& b;
+      ~Free() {
+        for (auto& x : b) (void)hipFree(x.first);
+      }
+    } guard{bufs};
+    ValidateParams v{};
+    v.K = K, v.O = O, v.H = H, v.R = R, v.noise = a->noise;
+    v.noise_level = a->noise_level, v.acc_const = a->acc_const_noise, v.steer_const = a->steer_const_noise;
+    v.K_steer = pc.K_steer, v.y_lb = pc.y_lb, v.y_ub = pc.y_ub, v.seed = a->seed;
+    v.Pdot = (const float*)up(basis.data(), kNum * kNvar * 4);
+    v.Pddot = (const float*)up(basis.data() + kNum * kNvar, kNum * kNvar * 4);
+    v.cx = (const double*)up(a->cx, size_t(K) * 11 * 8);
+    v.cy = (const double*)up(a->cy, size_t(K) * 11 * 8);
+    v.init_state = (const double*)up(a->init_state, size_t(K) * 6 * 8);
+    v.x_obs = (const float*)up(a->x_obs, size_t(K) * O * 100 * 4);
+    v.y_obs = (const float*)up(a->y_obs, size_t(K) * O * 100 * 4);
+    v.draws = a->draws ? (const double*)up(a->draws, size_t(K) * 3 * R * H * 8) : nullptr;
+    v.keys = (const uint32_t*)up(a->keys, size_t(K) * 4);
+    v.count = (int32_t*)up(nullptr, size_t(K) * 4);
+    v.count_lane = (int32_t*)up(nullptr, size_t(K) * 4);
+    launch_validate(v, nullptr);
+    HIPC(hipGetLastError());
+    HIPC(hipDeviceSynchronize());
+    HIPC(hipMemcpy(a->count, v.count, size_t(K) * 4, hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(a->count_lane, v.count_lane, size_t(K) * 4, hipMemcpyDeviceToHost));
+    return MPCMMD_OK;
+  });
+}
+
 int mpcmmd_obs_dynamic_traj(int32_t num_obs, const float* x0, const float* y0, const float* vx0, const float* vy0,
                             const float* v_des, float y_des, float* x_traj, float* y_traj) {
   if (num_obs < 0) return fail(MPCMMD_E_INVALID, "num_obs < 0");

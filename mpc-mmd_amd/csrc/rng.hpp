@@ -22,6 +22,13 @@ enum Stream : uint32_t {
   kStreamGammaAccB = 5,
   kStreamGammaSteerA = 6,
   kStreamGammaSteerB = 7,
+  kStreamValAcc = 24,  // validation (k_validate): normals acc / steer / const, Beta gammas
+  kStreamValSteer = 25,
+  kStreamValConst = 26,
+  kStreamValGammaAccA = 27,
+  kStreamValGammaAccB = 28,
+  kStreamValGammaSteerA = 29,
+  kStreamValGammaSteerB = 30,
   kStreamPop0 = 16,
   kStreamBetaZ0 = 17,
   kStreamBetaZ = 18,

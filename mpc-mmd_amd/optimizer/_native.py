@@ -25,7 +25,7 @@ SYMBOLS = (
     "mpcmmd_destroy", "mpcmmd_set_stream", "mpcmmd_get_stream", "mpcmmd_solve", "mpcmmd_begin",
     "mpcmmd_iterate", "mpcmmd_finish", "mpcmmd_sync", "mpcmmd_profile", "mpcmmd_kernel_times",
     "mpcmmd_kernel_name", "mpcmmd_buffer_info", "mpcmmd_read", "mpcmmd_write", "mpcmmd_run_stage",
-    "mpcmmd_host_constant", "mpcmmd_obs_dynamic_traj",
+    "mpcmmd_host_constant", "mpcmmd_obs_dynamic_traj", "mpcmmd_validate",
 )
 
 
@@ -47,6 +47,18 @@ class Result(C.Structure):
                 ("cost_obs", C.c_float), ("sigma", C.c_float), ("res_beta", C.c_float * 20),
                 ("beta", C.POINTER(C.c_float)), ("elite_proj", C.POINTER(C.c_int32)),
                 ("elite_obs", C.POINTER(C.c_int32)), ("elite_cem", C.POINTER(C.c_int32))]
+
+
+class ValidateArgs(C.Structure):
+    _fields_ = [("num_cfg", C.c_int32), ("num_obs", C.c_int32), ("num_prime", C.c_int32),
+                ("num_rollouts", C.c_int32), ("noise", C.c_int32), ("variant", C.c_int32),
+                ("noise_level", C.c_double), ("acc_const_noise", C.c_double), ("steer_const_noise", C.c_double),
+                ("seed", C.c_uint32), ("device", C.c_int32),
+                ("cx", C.POINTER(C.c_double)), ("cy", C.POINTER(C.c_double)),
+                ("init_state", C.POINTER(C.c_double)), ("x_obs", C.POINTER(C.c_float)),
+                ("y_obs", C.POINTER(C.c_float)), ("draws", C.POINTER(C.c_double)),
+                ("keys", C.POINTER(C.c_uint32)), ("count", C.POINTER(C.c_int32)),
+                ("count_lane", C.POINTER(C.c_int32))]
 
 
 class NativeError(RuntimeError):
@@ -91,6 +103,7 @@ def lib():
     L.mpcmmd_write.argtypes = [vp, C.c_char_p, vp, C.c_size_t]
     L.mpcmmd_run_stage.argtypes = [vp, C.c_int32, C.c_int32]
     L.mpcmmd_host_constant.argtypes = [C.POINTER(Config), C.c_char_p, C.POINTER(C.c_double), C.c_size_t]
+    L.mpcmmd_validate.argtypes = [C.POINTER(ValidateArgs)]
     L.mpcmmd_obs_dynamic_traj.argtypes = [C.c_int32, fp, fp, fp, fp, fp, C.c_float, fp, fp]
     if L.mpcmmd_abi_version() != ABI_VERSION:
         raise NativeError("libmpcmmd ABI version mismatch")
@@ -130,6 +143,34 @@ def obs_dynamic_traj(x0, y0, vx0, vy0, v_des, y_des=-1.75):
     yt = np.empty((O, 100), np.float32)
     check(lib().mpcmmd_obs_dynamic_traj(O, *[_fptr(v) for v in a], float(y_des), _fptr(xt), _fptr(yt)))
     return xt, yt
+
+
+def validate(cx, cy, init_state, x_obs, y_obs, keys, num_prime, noise, noise_level, acc_const_noise=0.0,
+             steer_const_noise=0.0, num_rollouts=1000, variant="static", draws=None, seed=0, device=0):
+    """mpcmmd_validate over K configurations: (count [K], count_lane [K])
+    (S/validation.py compute_stats :134-171).  cx, cy [K,11]; init_state
+    [K,6]; x_obs, y_obs [K,O,100] obstacle tracks; keys [K]; draws
+    [K,3,R,H] fp64 or None (internal Philox)."""
+    d = lambda a, *shape: np.ascontiguousarray(np.asarray(a, np.float64).reshape(*shape))
+    cx = np.atleast_2d(np.asarray(cx, np.float64))
+    K = cx.shape[0]
+    cx, cy = d(cx, K, 11), d(cy, K, 11)
+    st = d(init_state, K, 6)
+    xo = np.ascontiguousarray(np.asarray(x_obs, np.float32).reshape(K, -1, 100))
+    yo = np.ascontiguousarray(np.asarray(y_obs, np.float32).reshape(K, -1, 100))
+    O = xo.shape[1]
+    ks = np.ascontiguousarray(np.asarray(keys, np.int64).reshape(K).astype(np.uint32))
+    dr = None if draws is None else d(draws, K, 3, num_rollouts, num_prime)
+    cnt = np.zeros(K, np.int32)
+    cl = np.zeros(K, np.int32)
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+    args = ValidateArgs(K, O, int(num_prime), int(num_rollouts), NOISE[noise], VARIANT[variant], float(noise_level),
+                        float(acc_const_noise), float(steer_const_noise), int(seed) & 0xFFFFFFFF, int(device),
+                        dp(cx), dp(cy), dp(st), _fptr(xo), _fptr(yo), None if dr is None else dp(dr),
+                        ks.ctypes.data_as(C.POINTER(C.c_uint32)), cnt.ctypes.data_as(C.POINTER(C.c_int32)),
+                        cl.ctypes.data_as(C.POINTER(C.c_int32)))
+    check(lib().mpcmmd_validate(C.byref(args)))
+    return cnt, cl
 
 
 def _fptr(a):
