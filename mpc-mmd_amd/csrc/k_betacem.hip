@@ -308,7 +308,7 @@ DEVI void select_rows(Row row, Out out, int first, int last, int stride, int M, 
 //   A: A[r][h]   B: B[h][r]   C/D register i: C[h + 4 i][r]
 typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int kSampleTiles = kBzCols / 16;  // 6 tiles of 16 sample columns (89 used)
-constexpr int kTilesPerWave = 2;
+constexpr int kTilesPerWave = 6;
 constexpr int kSampleWaves = kSampleTiles / kTilesPerWave;
 static_assert(kSampleTiles % kTilesPerWave == 0, "tiles per wave");
 static_assert(kBzCols >= kNew, "sample tiles");
