@@ -89,15 +89,16 @@ def kernel_work(w, name, launches, stats):
     return None
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC pass
-    (profiles/r01_pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE per the
-    MI355X guide's gfx950 correction), or None."""
+def pmc_traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` in `workload` from the committed PMC
+    passes (profiles/r01_pmc_traffic.json, {workload: {kernel: bytes}}:
+    2 x FETCH_SIZE + WRITE_SIZE per the MI355X guide's gfx950 correction),
+    or None."""
     path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(kernel)
-    except (OSError, ValueError):
+            return json.load(f).get(workload, {}).get(kernel)
+    except (OSError, ValueError, AttributeError):
         return None
 
 
@@ -266,7 +267,7 @@ def main():
             roof["frac"] = roof["achieved"] / peak
             if model[0] == "ops64":
                 roof["bound"] = "valu-fp64"
-        roof["traffic"] = pmc_traffic(dom)
+        roof["traffic"] = pmc_traffic(a.workload, dom)
         roof["kernel"] = dom
         roof["avg_us"] = avg_s * 1e6
         line = {
