@@ -111,6 +111,37 @@ def run_block(prob, cost, ids, init_state, mean, cov, v_des=15.0, solve=None):
     return np.stack(rows) if rows else np.zeros((0, row_width(prob.num_reduced)), np.float32)
 
 
+def result_tuple(cost, r, num_reduced):
+    """Handle.finish() dict -> the compute_cem_* return tuple (cem.py:333 / 462)."""
+    if cost == "mmd_opt":
+        return (r["cx"], r["cy"], r["cost_lane"], r["cost_obs"], r["beta"][:num_reduced].copy(), r["sigma"],
+                r["res_beta"])
+    return r["cx"], r["cy"], r["cost_lane"], r["cost_obs"]
+
+
+def run_block_concurrent(prob, handles, cost, ids, init_state, mean, cov, v_des=15.0):
+    """Solve configs ``ids`` with len(handles) configurations in flight at
+    once (handles: native handles of prob's configuration, e.g. prob.handle
+    plus more).  Each handle owns its device buffers and a non-blocking HIP
+    stream; begin + iterate only enqueue work, so the kernels of up to G
+    configurations overlap on the GPU (the reference's num_batch = 100 fills
+    only 100 of the 256 CUs per launch).  Rows are identical to run_block's:
+    every configuration's RNG is keyed by its own idx_mpc."""
+    rows = []
+    G = len(handles)
+    ids = list(ids)
+    for g0 in range(0, len(ids), G):
+        group = ids[g0:g0 + G]
+        for h, k in zip(handles, group):
+            ob = static_obstacles(k, prob.num_obs)
+            xo, yo, _ = prob.cem_helper.compute_obs_trajectories(ob["x"], ob["y"], ob["vx"], ob["vy"], ob["psi"])
+            h.begin(cost, ob["idx_mpc"], init_state, mean, cov, xo, yo, v_des)
+            h.iterate(0, h.cfg.maxiter_cem)
+        for h, k in zip(handles, group):
+            rows.append(pack(k, result_tuple(cost, h.finish(), prob.num_reduced), prob.num_reduced))
+    return np.stack(rows) if rows else np.zeros((0, row_width(prob.num_reduced)), np.float32)
+
+
 def save_npz(path, rows, cost, num_obs, init_state):
     """Successful configs in the reference's layout (S/main_mpc.py:130-135)."""
     ok = rows[:, 2 + 2 * NV] <= threshold(cost)
@@ -137,6 +168,7 @@ def main():
     ap.add_argument("--acc-const-noise", type=float, default=0.0)
     ap.add_argument("--steer-const-noise", type=float, default=0.0)
     ap.add_argument("--out", default="")
+    ap.add_argument("--streams", type=int, default=8, help="configurations in flight per GPU (1 = one at a time)")
     a = ap.parse_args()
 
     import torch
@@ -156,7 +188,13 @@ def main():
     init = np.array([0.0, 1.75, 5.0, 0.0, 0.0, 0.0], np.float32)       # S/main_mpc.py:46-54
     mean = np.array([15.0] * 4 + [0.0] * 4, np.float32)                 # :56-71
     cov = np.diag([20.0] * 4 + [100.0] * 4).astype(np.float32)          # :69-74
-    rows = run_block(prob, a.cost, shard(a.num_configs, world, rank), init, mean, cov)
+    ids = shard(a.num_configs, world, rank)
+    if a.streams > 1:
+        from . import _native
+        hs = [prob.handle] + [_native.Handle(prob._cfg) for _ in range(a.streams - 1)]
+        rows = run_block_concurrent(prob, hs, a.cost, ids, init, mean, cov)
+    else:
+        rows = run_block(prob, a.cost, ids, init, mean, cov)
     allr = gather_rows(rows, a.num_configs, device if world > 1 else None)
     if rank == 0:
         out = a.out or "./data/{}_noise/noise_{}/ts_{}/{}_{}_samples_{}_obs".format(
