@@ -930,7 +930,12 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
     double s = 0.0;
     for (int q = 0; q < kBetaElite; ++q) s = s + double(Enew[size_t(q) * M1 + j]);
     const double m = s / double(kBetaElite);
-    for (int q = 0; q < kBetaElite; ++q) Ul[j * 11 + q] = (double(Enew[size_t(q) * M1 + j]) - m) * rs10;
+    double* gj = gen + size_t(j) * kGenStride + kGenU;
+    for (int q = 0; q < kBetaElite; ++q) {
+      const double u = (double(Enew[size_t(q) * M1 + j]) - m) * rs10;
+      Ul[j * 11 + q] = u;
+      gj[q] = u;
+    }
     p.genm[size_t(b) * pos_pad(M) + j] = double(float(m));
   }
   __syncthreads();
@@ -959,15 +964,48 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
     }
     c += a;
     double acc = a == c ? 1.0 : 0.0;
+    double* ph = p.phib + size_t(b) * nblk * 66;
     for (int blk = 0; blk < nblk; ++blk) {
       const double g = Gb[blk * 66 + tid];
-      Gb[blk * 66 + tid] = acc;
+      ph[blk * 66 + tid] = acc;
       acc = fma(g, kInvRidge, acc);
     }
   }
+  // last iteration: beta_best / reduced set of argmin (pre-update) and, when
+  // argmin is a carried elite, sigma_best (Q4); k_bsigma handles a new sample
+  if (last) {
+    const int* bsel = p.bsel + (size_t(b) * kBetaSamples + imin) * n;
+    for (int i = tid; i < n; i += blockDim.x) {
+      p.bestsel[size_t(b) * n + i] = bsel[i];
+      p.beta[size_t(b) * n + i] = p.btop[(size_t(b) * kBetaSamples + imin) * n + i];
+    }
+    if (tid == 0) {
+      p.bimin[b] = imin;
+      if (imin < kBetaElite) p.sigma[b] = Enew[size_t(imin) * M1 + M];
+    }
+  }
+}
+
+// k_bgen: level 2 of the generators, one thread per position j (no
+// cross-thread dependency): Phi_j = the block prefix (k_belite) + the
+// rank-1 terms of the earlier positions of j's block, its Cholesky,
+// v = Phi_j^-1 u_j, L_jj = sqrt(0.05 + u_j . v), w_j = v / L_jj.
+// Separate from k_belite so that kernel's LDS-bound phases are not held to
+// this phase's register count (184 VGPRs).
+__global__ __launch_bounds__(64) void k_bgen(Params p) {
+  __shared__ double us[64 * 11];  // u of this workgroup's 64 positions (whole 16-blocks)
+  const int b = blockIdx.y, M = p.M, M1 = M + 1;
+  const int j0 = blockIdx.x * 64, j = j0 + threadIdx.x;
+  const int nblk = (M1 + 15) / 16;
+  double* gen = p.gen + size_t(b) * pos_pad(M) * kGenStride;
+  const double* Gb = p.phib + size_t(b) * nblk * 66;
+  for (int i = threadIdx.x; i < 64 * 11; i += 64) {
+    const int r = i / 11, a = i - r * 11;
+    us[i] = j0 + r < M1 ? gen[size_t(j0 + r) * kGenStride + kGenU + a] : 0.0;
+  }
   __syncthreads();
-  // level 2: per position Phi_j, Cholesky, v = Phi^-1 u_j, L_jj, w_j
-  for (int j = tid; j < M1; j += blockDim.x) {
+  if (j >= M1) return;
+  {
     const int blk = j >> 4;
     double A[66];
 #pragma unroll
@@ -975,7 +1013,7 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
     for (int k = blk * 16; k < j; ++k) {
       double uk[11];
 #pragma unroll
-      for (int a = 0; a < 11; ++a) uk[a] = Ul[k * 11 + a];
+      for (int a = 0; a < 11; ++a) uk[a] = us[(k - j0) * 11 + a];
 #pragma unroll
       for (int a = 0; a < 11; ++a) {
         const double ua = uk[a] * kInvRidge;
@@ -1003,7 +1041,7 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
     }
     double u[11], v[11];
 #pragma unroll
-    for (int a = 0; a < 11; ++a) u[a] = Ul[j * 11 + a];
+    for (int a = 0; a < 11; ++a) u[a] = us[threadIdx.x * 11 + a];
     // R^T y = u
 #pragma unroll
     for (int a = 0; a < 11; ++a) {
@@ -1027,27 +1065,21 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
     const double rl = 1.0 / ljj;
     double* g = gen + size_t(j) * kGenStride;
 #pragma unroll
-    for (int a = 0; a < 11; ++a) {
-      g[kGenW + a] = v[a] * rl;
-      g[kGenU + a] = u[a];
-    }
+    for (int a = 0; a < 11; ++a) g[kGenW + a] = v[a] * rl;
     g[kGenL] = ljj;
   }
-  if (!last) return;
-  __syncthreads();
-  // last iteration: beta_best / reduced set of argmin (pre-update), sigma_best
-  // from the post-update samples at the same row (Q4, compute_beta.py:133-145)
-  const int* bsel = p.bsel + (size_t(b) * kBetaSamples + imin) * n;
-  for (int i = tid; i < n; i += blockDim.x) {
-    p.bestsel[size_t(b) * n + i] = bsel[i];
-    p.beta[size_t(b) * n + i] = p.btop[(size_t(b) * kBetaSamples + imin) * n + i];
-  }
-  if (imin < kBetaElite) {
-    if (tid == 0) p.sigma[b] = Enew[size_t(imin) * M1 + M];
-  } else {
-    // sigma coordinate of new sample imin-11 drawn with the NEW generators:
-    // y_M = mean_M + L_MM z_M + u_M . sum_{j<M} w_j z_j
-    double* red = reinterpret_cast<double*>(smem + C.Gb);  // reuse
+}
+
+// k_bsigma (last beta-iteration only): sigma_best when argmin is a new
+// sample -- its sigma coordinate drawn with the NEW generators (Q4,
+// compute_beta.py:133-145): y_M = mean_M + L_MM z_M + u_M . sum_{j<M} w_j z_j
+__global__ __launch_bounds__(kThreads) void k_bsigma(Params p, int tb) {
+  __shared__ double red[(kThreads / 64) * 11];
+  const int b = blockIdx.x, M = p.M, tid = threadIdx.x;
+  const int imin = p.bimin[b];
+  if (imin < kBetaElite) return;  // k_belite wrote it
+  const double* gen = p.gen + size_t(b) * pos_pad(M) * kGenStride;
+  {
     const double* z = p.beta_z + size_t(tb) * pos_pad(M) * kBzCols;
     const int si = imin - kBetaElite;
     double part[11];
@@ -1196,6 +1228,8 @@ void launch_bkernel(const Params& p, int tb, hipStream_t s) {
 void launch_belite(const Params& p, int tb, hipStream_t s) {
   const EliteLds e = elite_lds(p.M + 1);
   hipLaunchKernelGGL(k_belite, dim3(p.B), dim3(kThreads), e.total, s, p, tb);
+  hipLaunchKernelGGL(k_bgen, dim3((p.M + 1 + 63) / 64, p.B), dim3(64), 0, s, p);
+  if (tb == kBetaIters - 1) hipLaunchKernelGGL(k_bsigma, dim3(p.B), dim3(kThreads), 0, s, p, tb);
 }
 
 void launch_mmdfinal(const Params& p, int t, hipStream_t s) {

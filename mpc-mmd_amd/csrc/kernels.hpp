@@ -88,6 +88,8 @@ struct Params {
   float* bcost;            // [B][100]     QP costs
   float* belite;           // [2][B][11][M+1] elite sample vectors (ping-pong)
   double* gen;             // [B][pos_pad(M)][kGenStride] W, L_jj, U (pad rows 0)
+  double* phib;            // [B][ceil((M+1)/16)][66] Phi at the start of each 16-position block
+  int32_t* bimin;          // [B] argmin sample of the last beta-iteration
   double* genm;            // [B][pos_pad(M)]  fp32-rounded elite mean, as fp64 (pad 0)
   int32_t* bestsel;        // [B][n]       reduced set of the best sample
   double* brow;            // [B][100][n]  K_mixed row sums (fp64)

@@ -389,6 +389,8 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
       const size_t Pp = pos_pad(h->M);
       p.gen = (double*)h->alloc("gen", size_t(B) * Pp * kGenStride * 8);
       p.genm = (double*)h->alloc("genm", size_t(B) * Pp * 8);
+      p.phib = (double*)h->alloc("phib", size_t(B) * ((h->M + 1 + 15) / 16) * 66 * 8);
+      p.bimin = (int32_t*)h->alloc("bimin", size_t(B) * 4);
       p.bestsel = (int32_t*)h->alloc("bestsel", size_t(B) * n * 4);
       p.brow = (double*)h->alloc("brow", size_t(B) * kBetaSamples * n * 8);
       p.bkred = (float*)h->alloc("bkred", size_t(B) * kBetaSamples * (n * (n - 1) / 2) * 4);
