@@ -108,10 +108,11 @@ HDI GammaAttempt gamma_attempt(uint32_t k0, uint32_t k1, uint32_t stream, uint32
 // candidate applies only its own (alpha-dependent) transform.  Layout
 // [stream 0..3][k][field 0..3][h][r] (r fastest: coalesced per sample row).
 constexpr int kGammaTabAttempts = 4;
+constexpr double kBoostLinMin = -600.0;  // exp(-600) ~ 1e-261: no underflow in G' U^(1/alpha)
 constexpr int kGammaTabStreams = 4;  // acc A, acc B, steer A, steer B
 HDI size_t gamma_tab_size(int S, int H) { return size_t(kGammaTabStreams) * kGammaTabAttempts * 4 * S * H; }
 
-// log G' for alpha' = alpha (+1 when alpha < 1) and the boost log-uniform,
+// G' for alpha' = alpha (+1 when alpha < 1) and the boost log-uniform,
 // from the table (attempts < kGammaTabAttempts) then Philox directly.
 struct MtConst {
   double d, c;
@@ -121,11 +122,11 @@ HDI MtConst mt_const(double alpha) {
   const double d = a1 - 1.0 / 3.0;
   return MtConst{d, 1.0 / sqrt(9.0 * d)};
 }
-DEVI void log_gamma_parts_tab(MtConst mc, const double* tab, int S, int H, int r, int h, uint32_t k0, uint32_t k1,
-                              uint32_t stream, uint32_t elem, double& lg, double& lub) {
+DEVI void gamma_parts_tab(MtConst mc, const double* tab, int S, int H, int r, int h, uint32_t k0, uint32_t k1,
+                          uint32_t stream, uint32_t elem, double& g, double& lub) {
   const double d = mc.d, c = mc.c;
   const size_t plane = size_t(S) * H, at = size_t(h) * S + r;
-  lg = log(d);
+  g = d;
   lub = 0.0;
   for (int k = 0; k < kGammaTabAttempts; ++k) {
     const double* t = tab + size_t(k) * 4 * plane + at;
@@ -134,20 +135,20 @@ DEVI void log_gamma_parts_tab(MtConst mc, const double* tab, int S, int H, int r
     if (v > 0.0) {
       const double v3 = v * v * v;
       if (mt_accept(x, t[plane], t[2 * plane], d, v3)) {
-        lg = log(d * v3);
+        g = d * v3;
         lub = t[3 * plane];
         return;
       }
     }
   }
   for (int k = kGammaTabAttempts; k < kGammaMaxAttempts; ++k) {
-    const GammaAttempt g = gamma_attempt(k0, k1, stream, elem, k);
-    const double v = 1.0 + c * g.x;
+    const GammaAttempt ga = gamma_attempt(k0, k1, stream, elem, k);
+    const double v = 1.0 + c * ga.x;
     if (v > 0.0) {
       const double v3 = v * v * v;
-      if (mt_accept(g.x, g.u, g.lu, d, v3)) {
-        lg = log(d * v3);
-        lub = g.lw;
+      if (mt_accept(ga.x, ga.u, ga.lu, d, v3)) {
+        g = d * v3;
+        lub = ga.lw;
         return;
       }
     }
@@ -163,11 +164,17 @@ DEVI float beta_draw_tab(double a, double b, double ra, double rb, MtConst mc_a,
                          uint32_t k1, uint32_t stream_a, uint32_t stream_b) {
   const uint32_t elem = uint32_t(r) * uint32_t(H) + uint32_t(h);
   double ga, ua, gb, ub;
-  log_gamma_parts_tab(mc_a, tab_a, S, H, r, h, k0, k1, stream_a, elem, ga, ua);
-  log_gamma_parts_tab(mc_b, tab_b, S, H, r, h, k0, k1, stream_b, elem, gb, ub);
+  gamma_parts_tab(mc_a, tab_a, S, H, r, h, k0, k1, stream_a, elem, ga, ua);
+  gamma_parts_tab(mc_b, tab_b, S, H, r, h, k0, k1, stream_b, elem, gb, ub);
   if (a == 0.0 && b == 0.0) return (ua * rb > ub * ra) ? 1.0f : 0.0f;
-  const double la = a < 1.0 ? ga + ua / a : ga;
-  const double lb = b < 1.0 ? gb + ub / b : gb;
+  // G = G' U^(1/alpha) for alpha < 1 (boost); linear space while the boost
+  // factors cannot underflow, log space otherwise
+  const double ba = a < 1.0 ? ua / a : 0.0, bb = b < 1.0 ? ub / b : 0.0;
+  if (ba > kBoostLinMin && bb > kBoostLinMin) {
+    const double Ga = ga * (a < 1.0 ? exp(ba) : 1.0), Gb = gb * (b < 1.0 ? exp(bb) : 1.0);
+    return float(Ga / (Ga + Gb));
+  }
+  const double la = log(ga) + ba, lb = log(gb) + bb;
   // exp(la - lm), exp(lb - lm) with lm = max(la, lb): one of them is exp(0) = 1 exactly
   if (la > lb) {
     const double eb = exp(lb - la);

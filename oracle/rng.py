@@ -38,6 +38,7 @@ STREAM_POP0, STREAM_BETA_Z0, STREAM_BETA_Z = 16, 17, 18
 FIXED_KEY0 = 0xFFFFFFFF
 GAMMA_MAX_ATTEMPTS = 32
 BETA_A_RATIO, BETA_B_RATIO = 2.0, 5.0   # beta_a, beta_b (S/opt/cem.py:24)
+BOOST_LIN_MIN = -600.0                  # csrc/rng.hpp: kBoostLinMin
 
 
 def philox4x32_10(ctr, key):
@@ -92,7 +93,7 @@ def fixed_key(seed):
     return (FIXED_KEY0, int(seed) & MASK)
 
 
-def _log_gamma_parts(alpha, key, stream, elem):
+def _log_gamma_parts(alpha, key, stream, elem, linear=False):
     """Marsaglia-Tsang core for Gamma(alpha') with alpha' = alpha + 1 when
     alpha < 1 (boost), in fp64.  Returns (log G', log U_boost).
 
@@ -102,13 +103,14 @@ def _log_gamma_parts(alpha, key, stream, elem):
     table of these same values (csrc/rng.hpp: k_gamma_tab); that is caching,
     not a different stream.
     Not accepted after GAMMA_MAX_ATTEMPTS -> G' = d (never observed).
+    ``linear=True`` returns G' itself instead of log G'.
     """
     alpha = np.asarray(alpha, dtype=np.float64)
     elem = np.asarray(elem, dtype=np.uint64)
     a1 = np.where(alpha < 1.0, alpha + 1.0, alpha)
     d = a1 - 1.0 / 3.0
     c = 1.0 / np.sqrt(9.0 * d)
-    out = np.log(d)
+    out = d.copy() if linear else np.log(d)
     logub = np.zeros(alpha.shape)
     done = np.zeros(alpha.shape, dtype=bool)
     for k in range(GAMMA_MAX_ATTEMPTS):
@@ -125,7 +127,7 @@ def _log_gamma_parts(alpha, key, stream, elem):
         squeeze = uu < 1.0 - 0.0331 * (x * x) * (x * x)
         acc = vpos & (squeeze | (lu < 0.5 * x * x + d - d * v3 + d * np.log(v3)))
         newly = acc & ~done
-        out = np.where(newly, np.log(d * v3), out)
+        out = np.where(newly, d * v3 if linear else np.log(d * v3), out)
         logub = np.where(newly, np.log(_u01(u[3])), logub)
         done = done | acc
         if done.all():
@@ -134,27 +136,35 @@ def _log_gamma_parts(alpha, key, stream, elem):
 
 
 def beta_draws(a, b, key, stream_a, stream_b, elem):
-    """Beta(a, b) = Ga / (Ga + Gb) evaluated in log space (fp64 -> fp32).
-
-    log G = log G' + log(U)/alpha for alpha < 1.  For a = b = 0 (|control| == 0
-    exactly) the reference's Beta(0, 0) is NaN; with the
-    reference's fp32 solves the controls are never exactly zero, so we take
-    the alpha -> 0+ limit of the same draw instead: 1 if
+    """Beta(a, b) = Ga / (Ga + Gb) (fp64 -> fp32), G = G' U^(1/alpha) for
+    alpha < 1 (boost).  Evaluated in linear space while both boost factors
+    log(U)/alpha exceed -600 (no underflow), else in log space -- the same
+    two-branch formula as csrc/rng.hpp: beta_draw_tab.  For a = b = 0
+    (|control| == 0 exactly) the reference's Beta(0, 0) is NaN (SURVEY Q11);
+    with the reference's fp32 solves the controls are never exactly zero, so
+    we take the alpha -> 0+ limit of the same draw instead: 1 if
     log(U_a)/a_ratio > log(U_b)/b_ratio else 0 (DESIGN.md, Numerics).
     """
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
-    ga, ua = _log_gamma_parts(a, key, stream_a, elem)
-    gb, ub = _log_gamma_parts(b, key, stream_b, elem)
+    ga, ua = _log_gamma_parts(a, key, stream_a, elem, linear=True)
+    gb, ub = _log_gamma_parts(b, key, stream_b, elem, linear=True)
     zero = (a == 0.0) & (b == 0.0)
     sa = np.where(a > 0, a, 1.0)
     sb = np.where(b > 0, b, 1.0)
-    la = np.where(a < 1.0, ga + ua / sa, ga)
-    lb = np.where(b < 1.0, gb + ub / sb, gb)
-    lm = np.maximum(la, lb)
-    ea = np.exp(la - lm)
-    eb = np.exp(lb - lm)
-    out = ea / (ea + eb)
+    ba = np.where(a < 1.0, ua / sa, 0.0)
+    bb = np.where(b < 1.0, ub / sb, 0.0)
+    with np.errstate(over="ignore", under="ignore", divide="ignore", invalid="ignore"):
+        Ga = ga * np.where(a < 1.0, np.exp(ba), 1.0)
+        Gb = gb * np.where(b < 1.0, np.exp(bb), 1.0)
+        lin = Ga / (Ga + Gb)
+        la = np.log(ga) + ba
+        lb = np.log(gb) + bb
+        lm = np.maximum(la, lb)
+        ea = np.exp(la - lm)
+        eb = np.exp(lb - lm)
+        logsp = ea / (ea + eb)
+    out = np.where((ba > BOOST_LIN_MIN) & (bb > BOOST_LIN_MIN), lin, logsp)
     lim = np.where(ua * BETA_B_RATIO > ub * BETA_A_RATIO, 1.0, 0.0)
     return np.where(zero, lim, out).astype(F32)
 
