@@ -139,6 +139,7 @@ __global__ __launch_bounds__(256) void k_gamma_tab(Params p, int t) {
   const int S = p.S, H = p.H;
   const int plane = S * H;
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx == 0) *p.bfix_n = 0u;  // k_beta_planes' deferred list of this iteration
   if (idx >= kGammaTabStreams * kGammaTabAttempts * plane) return;
   const int e = idx % plane, sk = idx / plane;
   const int k = sk % kGammaTabAttempts, st = sk / kGammaTabAttempts;
@@ -167,17 +168,46 @@ __global__ __launch_bounds__(256) void k_beta_planes(Params p, int t) {
   }
   __syncthreads();
   if (r >= S) return;
+  // table-only fast path; the rare rest (more than the tabulated attempts)
+  // is deferred to k_beta_fix so this kernel does not carry that code's registers
+  const size_t sl = size_t(kGammaTabAttempts) * 4 * S * H;
+  const float fa = fabsf(a), fs = fabsf(st);
   float nba, nbs;
-  beta_pair(p, t, r, h, a, st, nba, nbs, mc);
+  const bool ok = beta_draw_fast(double(2.0f * fa), double(5.0f * fa), 2.0, 5.0, mc[0], mc[1], p.gtab, p.gtab + sl,
+                                 S, H, r, h, nba) &&
+                  beta_draw_fast(double(2.0f * fs), double(5.0f * fs), 2.0, 5.0, mc[2], mc[3], p.gtab + 2 * sl,
+                                 p.gtab + 3 * sl, S, H, r, h, nbs);
+  if (!ok) {
+    const unsigned slot = atomicAdd(p.bfix_n, 1u);
+    p.bfix[slot] = (uint32_t(b) * uint32_t(H) + uint32_t(h)) * uint32_t(S) + uint32_t(r);
+    return;
+  }
   float* o = p.bplane + size_t(b) * 2 * H * S;
   o[size_t(h) * S + r] = nba;
   o[(size_t(H) + h) * S + r] = nbs;
+}
+
+// the deferred elements of k_beta_planes, through the full sampler
+__global__ __launch_bounds__(256) void k_beta_fix(Params p, int t) {
+  const int S = p.S, H = p.H;
+  const unsigned cnt = *p.bfix_n;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
+    const uint32_t e = p.bfix[i];
+    const int r = int(e % uint32_t(S)), bh = int(e / uint32_t(S));
+    const int h = bh % H, b = bh / H;
+    float nba, nbs;
+    beta_pair(p, t, r, h, p.acc[size_t(b) * 100 + h], p.steer[size_t(b) * 100 + h], nba, nbs);
+    float* o = p.bplane + size_t(b) * 2 * H * S;
+    o[size_t(h) * S + r] = nba;
+    o[(size_t(H) + h) * S + r] = nbs;
+  }
 }
 
 }  // namespace
 
 void launch_beta_planes(const Params& p, int t, hipStream_t s) {
   hipLaunchKernelGGL(k_beta_planes, dim3((p.S + 255) / 256, p.H, p.B), dim3(256), 0, s, p, t);
+  hipLaunchKernelGGL(k_beta_fix, dim3(256), dim3(256), 0, s, p, t);
 }
 
 void launch_gamma_tab(const Params& p, int t, hipStream_t s) {

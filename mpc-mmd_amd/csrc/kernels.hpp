@@ -55,6 +55,8 @@ struct Params {
   const float* roll;       // [T][3][H][S]
   const float* resample;   // [T][B-5][8]
   float* bplane;           // [B][2][H][S] Beta draws (acc, steer) of the baseline rollouts (beta noise)
+  uint32_t* bfix;          // [B*H*S] elements k_beta_planes deferred to k_beta_fix
+  uint32_t* bfix_n;        // their count (zeroed by k_gamma_tab)
   double* gtab;            // Beta-noise attempt table of the current iteration (rng.hpp: gamma_tab_size)
   const float* beta_z0;    // [100][M+1]
   const double* beta_z;    // [20][pos_pad(M)][kBzCols] fp32 normals held as fp64 (position-major, zero padded)

@@ -373,6 +373,8 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
     p.roll = (const float*)h->alloc("roll", size_t(T) * 3 * H * S * 4);
     p.resample = (const float*)h->alloc("resample", size_t(T) * (B - kElite) * 8 * 4);
     p.bplane = (float*)h->alloc("bplane", c.noise == MPCMMD_NOISE_BETA ? size_t(B) * 2 * H * S * 4 : 16);
+    p.bfix = (uint32_t*)h->alloc("bfix", c.noise == MPCMMD_NOISE_BETA ? size_t(B) * H * S * 4 : 16);
+    p.bfix_n = (uint32_t*)h->alloc("bfix_n", 16);
     p.gtab = (double*)h->alloc("gtab", c.noise == MPCMMD_NOISE_BETA ? gamma_tab_size(S, H) * 8 : 16);
     if (mmd_ok) {
       p.beta_z0 = (const float*)h->alloc("beta_z0", size_t(kBetaSamples) * (h->M + 1) * 4);

@@ -184,4 +184,50 @@ DEVI float beta_draw_tab(double a, double b, double ra, double rb, MtConst mc_a,
   return float(ea / (ea + 1.0));
 }
 
+// Table-only fast path of beta_draw_tab for the hot plane kernel: returns
+// false (and leaves `out`) when a gamma needs more than the tabulated
+// attempts (rare); the caller then defers
+// the element to the full beta_draw_tab (identical arithmetic).
+DEVI bool gamma_tab_only(MtConst mc, const double* tab, size_t plane, size_t at, double& g, double& lub) {
+  for (int k = 0; k < kGammaTabAttempts; ++k) {
+    const double* t = tab + size_t(k) * 4 * plane + at;
+    const double x = t[0];
+    const double v = 1.0 + mc.c * x;
+    if (v > 0.0) {
+      const double v3 = v * v * v;
+      if (mt_accept(x, t[plane], t[2 * plane], mc.d, v3)) {
+        g = mc.d * v3;
+        lub = t[3 * plane];
+        return true;
+      }
+    }
+  }
+  return false;
+}
+DEVI bool beta_draw_fast(double a, double b, double ra, double rb, MtConst mc_a, MtConst mc_b, const double* tab_a,
+                         const double* tab_b, int S, int H, int r, int h, float& out) {
+  const size_t plane = size_t(S) * H, at = size_t(h) * S + r;
+  double ga, ua, gb, ub;
+  if (!gamma_tab_only(mc_a, tab_a, plane, at, ga, ua) || !gamma_tab_only(mc_b, tab_b, plane, at, gb, ub))
+    return false;
+  if (a == 0.0 && b == 0.0) {
+    out = (ua * rb > ub * ra) ? 1.0f : 0.0f;
+    return true;
+  }
+  const double ba = a < 1.0 ? ua / a : 0.0, bb = b < 1.0 ? ub / b : 0.0;
+  if (ba > kBoostLinMin && bb > kBoostLinMin) {
+    const double Ga = ga * (a < 1.0 ? exp(ba) : 1.0), Gb = gb * (b < 1.0 ? exp(bb) : 1.0);
+    out = float(Ga / (Ga + Gb));
+    return true;
+  }
+  const double la = log(ga) + ba, lb = log(gb) + bb;
+  if (la > lb) {
+    out = float(1.0 / (1.0 + exp(lb - la)));
+  } else {
+    const double ea = exp(la - lb);
+    out = float(ea / (ea + 1.0));
+  }
+  return true;
+}
+
 }  // namespace mpcmmd
