@@ -59,7 +59,7 @@ struct ReduceScratch {
 // jnp.quantile(x, 0.98) (linear, JAX fp32 weights) + mean of the tail
 // (costs.py:215-219) over vals[0..S).  list: >= S ints of LDS scratch.
 // Sorted order = the jnp.argsort total order (ties by index).
-DEVI float block_cvar(const float* vals, int S, int* list, ReduceScratch& rs) {
+DEVI float block_cvar(const float* vals, int S, unsigned long long* list, ReduceScratch& rs) {
   const float pos = 0.98f * float(S - 1);
   const float flo = floorf(pos), fhi = ceilf(pos);
   const float hw = pos - flo;
@@ -67,14 +67,16 @@ DEVI float block_cvar(const float* vals, int S, int* list, ReduceScratch& rs) {
   const int lo = min(max(int(flo), 0), S - 1), hi = min(max(int(fhi), 0), S - 1);
   if (threadIdx.x == 0) rs.list_n = 0;
   __syncthreads();
-  // zero class (key of +-0) sorts first: count it, compact the rest
+  // zero class (key of +-0) sorts first: count it, compact the rest as
+  // (sort key, index) pairs -- their 64-bit order is the stable argsort's
   int nz = 0;
   for (int s = threadIdx.x; s < S; s += blockDim.x) {
-    if (sort_key(vals[s]) == 0x80000000u) {
+    const uint32_t k = sort_key(vals[s]);
+    if (k == 0x80000000u) {
       ++nz;
     } else {
       const int slot = atomicAdd(&rs.list_n, 1);
-      list[slot] = s;
+      list[slot] = (static_cast<unsigned long long>(k) << 32) | static_cast<unsigned>(s);
     }
   }
   const int z = block_sum(nz, rs.i);  // also a barrier
@@ -86,14 +88,11 @@ DEVI float block_cvar(const float* vals, int S, int* list, ReduceScratch& rs) {
   __syncthreads();
   if (hi >= z) {
     for (int a = threadIdx.x; a < m; a += blockDim.x) {
-      const int ia = list[a];
-      const uint32_t ka = sort_key(vals[ia]);
+      const unsigned long long ka = list[a];
       int r = 0;
-      for (int c = 0; c < m; ++c) {
-        const int ic = list[c];
-        const uint32_t kc = sort_key(vals[ic]);
-        r += (kc < ka) || (kc == ka && ic < ia);
-      }
+#pragma unroll 8
+      for (int c = 0; c < m; ++c) r += list[c] < ka;  // LDS broadcast reads
+      const int ia = int(ka & 0xFFFFFFFFull);
       if (r == lo - z) rs.v_lo = vals[ia];
       if (r == hi - z) rs.v_hi = vals[ia];
     }

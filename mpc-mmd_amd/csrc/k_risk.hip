@@ -31,7 +31,7 @@ struct RiskLds {
   float* cbar;
   float* lb;
   float* ub;
-  int* list;
+  unsigned long long* list;
   ReduceScratch* rs;
 };
 
@@ -52,9 +52,10 @@ DEVI RiskLds carve(char* base, int O, int H, int S) {
   f += S;
   L.ub = f;
   f += S;
-  L.list = reinterpret_cast<int*>(f);
-  f += S;
   size_t off = size_t(reinterpret_cast<char*>(f) - base);
+  off = (off + 15) & ~size_t(15);
+  L.list = reinterpret_cast<unsigned long long*>(base + off);
+  off += size_t(S) * 8;
   off = (off + 15) & ~size_t(15);
   L.rs = reinterpret_cast<ReduceScratch*>(base + off);
   return L;
@@ -63,7 +64,9 @@ DEVI RiskLds carve(char* base, int O, int H, int S) {
 }  // namespace
 
 size_t risk_lds_bytes(int O, int H, int S) {
-  size_t f = size_t(2 * O * H + 2 * H + 4 * S) * 4;
+  size_t f = size_t(2 * O * H + 2 * H + 3 * S) * 4;
+  f = (f + 15) & ~size_t(15);
+  f += size_t(S) * 8;  // (key, index) pairs of block_cvar
   f = (f + 15) & ~size_t(15);
   return f + sizeof(ReduceScratch);
 }
