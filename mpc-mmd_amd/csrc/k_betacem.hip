@@ -116,9 +116,19 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
 constexpr int kDistRows = 32;
 constexpr int kDistThreads = 256;
 
+// XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs by
+// linear id, so id L runs on XCD L % 8.  Candidate b's row tiles get ids
+// ((b / 8) * T + tile) * 8 + b % 8: all on one XCD and launched together, so
+// the candidate's column features (42 KB) are read from HBM once and then
+// hit that XCD's L2, instead of once per tile.
+constexpr int kXcds = 8;
+
 __global__ __launch_bounds__(kDistThreads) void k_bdist(Params p) {
   __shared__ __attribute__((aligned(16))) float Fr[kDistRows][kF + 2];
-  const int b = blockIdx.x, r0 = blockIdx.y * kDistRows, M = p.M, Md = dist_stride(M);
+  const int M = p.M, Md = dist_stride(M), T = (M + kDistRows - 1) / kDistRows;
+  const int L = blockIdx.x, q = L / kXcds;
+  const int b = (q / T) * kXcds + L % kXcds, r0 = (q % T) * kDistRows;
+  if (b >= p.B) return;
   const int tid = threadIdx.x;
   const float* Fg = p.feat + size_t(b) * kF * M;
   for (int i = tid; i < kDistRows * kF; i += kDistThreads) {
@@ -1188,7 +1198,8 @@ void launch_mother(const Params& p, int t, hipStream_t s) {
 }
 
 void launch_bdist(const Params& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_bdist, dim3(p.B, (p.M + kDistRows - 1) / kDistRows), dim3(kDistThreads), 0, s, p);
+  const int T = (p.M + kDistRows - 1) / kDistRows, groups = (p.B + kXcds - 1) / kXcds;
+  hipLaunchKernelGGL(k_bdist, dim3(groups * T * kXcds), dim3(kDistThreads), 0, s, p);
 }
 
 void launch_bsample(const Params& p, int tb, hipStream_t s) {
