@@ -598,9 +598,12 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb, int b
   for (int c0 = 0; c0 < U; c0 += R) {
     const int rc = min(R, U - c0);
     __syncthreads();  // previous chunk consumed (and, first time, pairs built)
+    // LDS-DMA (global_load_lds_dwordx4): the chunk image is lane-linear (rows
+    // contiguous, no padding), each lane's source row is its own address
     for (int idx = tid; idx < rc * q4; idx += kKerThreads) {
       const int u = idx / q4, c = idx - u * q4;
-      reinterpret_cast<float4*>(Dl)[idx] = Dg[size_t(ulist[c0 + u]) * q4 + c];
+      __builtin_amdgcn_global_load_lds(Dg + size_t(ulist[c0 + u]) * q4 + c,
+                                       reinterpret_cast<float4*>(Dl) + (idx - (tid & 63)), 16, 0, 0);
     }
     __syncthreads();
     if (c0 == 0) MPCMMD_STAMP(p, 18);
