@@ -519,7 +519,7 @@ constexpr size_t kLdsBudget = 160 * 1024 - 1024;
 // k_bkernel runs two workgroups per CU (one's D-row loads overlap the
 // other's exp sums) whenever half the LDS still holds this many D rows
 constexpr size_t kKerHalfBudget = 80 * 1024;
-constexpr int kKerMinRowsHalf = 16;
+constexpr int kKerMinRowsHalf = 8;
 constexpr float kNegLog2e = -1.44269504088896340736f;
 
 __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb, int budget) {
