@@ -46,6 +46,24 @@ def static_obstacles(k: int, num_obs: int):
     return dict(x=x, y=y, vx=z, vy=z.copy(), psi=z.copy(), idx_mpc=idx_mpc)
 
 
+def obstacles(variant: str, k: int, num_obs: int):
+    """Configuration k of the static (S/main_mpc.py:10-21) or dynamic
+    (synthetic_dynamic_obs/main_mpc.py:108-126, QP obstacle tracks in
+    ``x_traj``/``y_traj``) driver."""
+    if variant == "dynamic":
+        from .obs_data_generate_dynamic import dynamic_obstacles
+        return dynamic_obstacles(k, num_obs)
+    return static_obstacles(k, num_obs)
+
+
+def tracks(prob, ob):
+    """x_obs_traj, y_obs_traj [O][100] of one configuration."""
+    if "x_traj" in ob:
+        return ob["x_traj"], ob["y_traj"]
+    xo, yo, _ = prob.cem_helper.compute_obs_trajectories(ob["x"], ob["y"], ob["vx"], ob["vy"], ob["psi"])
+    return xo, yo
+
+
 def row_width(num_reduced: int) -> int:
     # id, cx, cy, cost_lane, cost_obs, sigma, res_beta[20], beta[n]
     return 1 + 2 * NV + 3 + 20 + num_reduced
@@ -97,7 +115,7 @@ def threshold(cost: str, ker_wt: float = 1000.0) -> float:
     return -ker_wt + 1.0 if cost in ("mmd_opt", "mmd_random") else 1e-5
 
 
-def run_block(prob, cost, ids, init_state, mean, cov, v_des=15.0, solve=None):
+def run_block(prob, cost, ids, init_state, mean, cov, v_des=15.0, solve=None, variant="static"):
     """Solve configs ``ids`` on this rank; ``solve(k, obs) -> out tuple``
     defaults to ``prob.compute_cem_<cost>``."""
     fn = solve
@@ -105,9 +123,9 @@ def run_block(prob, cost, ids, init_state, mean, cov, v_des=15.0, solve=None):
         meth = getattr(prob, f"compute_cem_{cost}")
 
         def fn(k, ob):
-            xo, yo, _ = prob.cem_helper.compute_obs_trajectories(ob["x"], ob["y"], ob["vx"], ob["vy"], ob["psi"])
+            xo, yo = tracks(prob, ob)
             return meth(ob["idx_mpc"], init_state, mean, cov, xo, yo, v_des)
-    rows = [pack(k, fn(k, static_obstacles(k, prob.num_obs)), prob.num_reduced) for k in ids]
+    rows = [pack(k, fn(k, obstacles(variant, k, prob.num_obs)), prob.num_reduced) for k in ids]
     return np.stack(rows) if rows else np.zeros((0, row_width(prob.num_reduced)), np.float32)
 
 
@@ -119,7 +137,7 @@ def result_tuple(cost, r, num_reduced):
     return r["cx"], r["cy"], r["cost_lane"], r["cost_obs"]
 
 
-def run_block_concurrent(prob, handles, cost, ids, init_state, mean, cov, v_des=15.0):
+def run_block_concurrent(prob, handles, cost, ids, init_state, mean, cov, v_des=15.0, variant="static"):
     """Solve configs ``ids`` with len(handles) configurations in flight at
     once (handles: native handles of prob's configuration, e.g. prob.handle
     plus more).  Each handle owns its device buffers and a non-blocking HIP
@@ -133,8 +151,8 @@ def run_block_concurrent(prob, handles, cost, ids, init_state, mean, cov, v_des=
     for g0 in range(0, len(ids), G):
         group = ids[g0:g0 + G]
         for h, k in zip(handles, group):
-            ob = static_obstacles(k, prob.num_obs)
-            xo, yo, _ = prob.cem_helper.compute_obs_trajectories(ob["x"], ob["y"], ob["vx"], ob["vy"], ob["psi"])
+            ob = obstacles(variant, k, prob.num_obs)
+            xo, yo = tracks(prob, ob)
             h.begin(cost, ob["idx_mpc"], init_state, mean, cov, xo, yo, v_des)
             h.iterate(0, h.cfg.maxiter_cem)
         for h, k in zip(handles, group):
@@ -142,16 +160,22 @@ def run_block_concurrent(prob, handles, cost, ids, init_state, mean, cov, v_des=
     return np.stack(rows) if rows else np.zeros((0, row_width(prob.num_reduced)), np.float32)
 
 
-def save_npz(path, rows, cost, num_obs, init_state):
-    """Successful configs in the reference's layout (S/main_mpc.py:130-135)."""
+def save_npz(path, rows, cost, num_obs, init_state, variant="static"):
+    """Successful configs in the reference's layout (S/main_mpc.py:130-135;
+    dynamic: D/main_mpc.py:150-156 adds psi_obs, x_obs_traj, y_obs_traj)."""
     ok = rows[:, 2 + 2 * NV] <= threshold(cost)
     ks = rows[ok, 0].astype(int)
-    obs = [static_obstacles(int(k), num_obs) for k in ks]
+    obs = [obstacles(variant, int(k), num_obs) for k in ks]
     stack = lambda key: np.array([o[key] for o in obs]).reshape(len(obs), num_obs)
+    extra = {}
+    if variant == "dynamic":
+        extra = dict(psi_obs=stack("psi"),
+                     x_obs_traj=np.array([o["x_traj"] for o in obs]).reshape(len(obs), num_obs, 100),
+                     y_obs_traj=np.array([o["y_traj"] for o in obs]).reshape(len(obs), num_obs, 100))
     os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
     np.savez(path, cx=rows[ok, 1:1 + NV].astype(np.float64), cy=rows[ok, 1 + NV:1 + 2 * NV].astype(np.float64),
              init_state=np.tile(np.asarray(init_state, np.float64), (len(ks), 1)),
-             x_obs=stack("x"), y_obs=stack("y"), vx_obs=stack("vx"), vy_obs=stack("vy"))
+             x_obs=stack("x"), y_obs=stack("y"), vx_obs=stack("vx"), vy_obs=stack("vy"), **extra)
     return int(ok.sum())
 
 
@@ -169,6 +193,7 @@ def main():
     ap.add_argument("--steer-const-noise", type=float, default=0.0)
     ap.add_argument("--out", default="")
     ap.add_argument("--streams", type=int, default=8, help="configurations in flight per GPU (1 = one at a time)")
+    ap.add_argument("--variant", default="static", choices=["static", "dynamic"])
     a = ap.parse_args()
 
     import torch
@@ -184,22 +209,23 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
     prob = CEM(a.num_reduced, a.num_obs, a.noise_level, a.num_prime, a.noise, a.acc_const_noise,
-               a.steer_const_noise, num_batch=a.num_batch, device=local)
-    init = np.array([0.0, 1.75, 5.0, 0.0, 0.0, 0.0], np.float32)       # S/main_mpc.py:46-54
+               a.steer_const_noise, num_batch=a.num_batch, device=local, variant=a.variant)
+    y0 = 1.75 if a.variant == "static" else -1.75                      # D/main_mpc.py:34-42
+    init = np.array([0.0, y0, 5.0, 0.0, 0.0, 0.0], np.float32)          # S/main_mpc.py:46-54
     mean = np.array([15.0] * 4 + [0.0] * 4, np.float32)                 # :56-71
     cov = np.diag([20.0] * 4 + [100.0] * 4).astype(np.float32)          # :69-74
     ids = shard(a.num_configs, world, rank)
     if a.streams > 1:
         from . import _native
         hs = [prob.handle] + [_native.Handle(prob._cfg) for _ in range(a.streams - 1)]
-        rows = run_block_concurrent(prob, hs, a.cost, ids, init, mean, cov)
+        rows = run_block_concurrent(prob, hs, a.cost, ids, init, mean, cov, variant=a.variant)
     else:
-        rows = run_block(prob, a.cost, ids, init, mean, cov)
+        rows = run_block(prob, a.cost, ids, init, mean, cov, variant=a.variant)
     allr = gather_rows(rows, a.num_configs, device if world > 1 else None)
     if rank == 0:
         out = a.out or "./data/{}_noise/noise_{}/ts_{}/{}_{}_samples_{}_obs".format(
             a.noise, int(a.noise_level * 100), a.num_prime, a.cost, a.num_reduced, a.num_obs)
-        nok = save_npz(out, allr, a.cost, a.num_obs, init)
+        nok = save_npz(out, allr, a.cost, a.num_obs, init, a.variant)
         print(f"{a.cost}: {nok}/{a.num_configs} configs meet the threshold -> {out}.npz")
     if world > 1:
         dist.destroy_process_group()

@@ -79,3 +79,24 @@ def test_gloo_world2_gather_equals_single_process(tmp_path, n):
     d = np.load(str(tmp_path / "d" / "mmd_opt_6_samples_4_obs.npz"))
     assert nok == sum(1 for k in range(n) if k % 3) == d["cx"].shape[0]
     assert sorted(d.files) == ["cx", "cy", "init_state", "vx_obs", "vy_obs", "x_obs", "y_obs"]
+
+
+def test_dynamic_variant_rows_and_npz(tmp_path):
+    """synthetic_dynamic_obs sweep (BASELINE configs[3] shape: num_obs = 20):
+    obstacle tracks from the library's QP flow into the solve, and the npz
+    carries the dynamic driver's extra keys (D/main_mpc.py:150-156)."""
+    seen = {}
+
+    def solve(k, ob):
+        seen[k] = ob["x_traj"]
+        return _fake_solve(k, ob)
+
+    class P(_Prob):
+        num_obs = 20
+
+    rows = sweep.run_block(P(), "mmd_opt", range(4), None, None, None, solve=solve, variant="dynamic")
+    assert rows.shape[0] == 4 and all(v.shape == (20, 100) for v in seen.values())
+    nok = sweep.save_npz(str(tmp_path / "dyn"), rows, "mmd_opt", 20, np.zeros(6), "dynamic")
+    d = np.load(str(tmp_path / "dyn.npz"))
+    assert nok == d["x_obs_traj"].shape[0] and d["x_obs_traj"].shape[1:] == (20, 100)
+    assert "psi_obs" in d and "y_obs_traj" in d
