@@ -80,6 +80,13 @@ struct mpcmmd_handle {
   bool beta_tables_internal = false;  // device beta tables hold the internal streams
   bool mmd_ok = false;                // mmd_opt buffers allocated (mmdopt_supported)
   std::string mmd_why;
+  // pinned staging for the per-solve uploads of mpcmmd_begin: the copies are
+  // asynchronous, so their source must outlive the call; the next begin waits
+  // for stage_ev before refilling it
+  char* stage = nullptr;
+  size_t stage_bytes = 0, stage_used = 0;
+  hipEvent_t stage_ev = nullptr;
+  bool stage_pending = false;
   // profiling
   bool prof = false;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -169,6 +176,25 @@ void upload(mpcmmd_handle* h, const char* name, const void* src, size_t bytes, s
   auto it = h->bufs.find(name);
   if (it == h->bufs.end() || offset + bytes > it->second.second) throw std::runtime_error(std::string("buffer ") + name);
   HIPC(hipMemcpyAsync(static_cast<char*>(it->second.first) + offset, src, bytes, hipMemcpyHostToDevice, h->stream));
+}
+
+// upload through the handle's pinned staging area (mpcmmd_begin): src may be
+// a host temporary, the copy still runs after the call returns
+void upload_staged(mpcmmd_handle* h, const char* name, const void* src, size_t bytes) {
+  const size_t at = (h->stage_used + 63) & ~size_t(63);
+  if (at + bytes > h->stage_bytes) throw std::runtime_error(std::string("staging area too small for ") + name);
+  std::memcpy(h->stage + at, src, bytes);
+  h->stage_used = at + bytes;
+  upload(h, name, h->stage + at, bytes);
+}
+
+// bytes of staging mpcmmd_begin needs at most (each piece 64-byte aligned)
+size_t stage_size(int B, int S, int H, int O, int T) {
+  const size_t pieces[] = {size_t(4) * 11 * 8, 8 * 4, size_t(2) * O * H * 4, size_t(B) * 8 * 4, 8 * 4, 64 * 4,
+                           size_t(T) * 3 * H * S * 4, size_t(T) * (B - kElite) * 8 * 4};
+  size_t s = 0;
+  for (size_t b : pieces) s += (b + 63) & ~size_t(63);
+  return s + 64;
 }
 
 // beta_z iteration t: [89][M+1] (draw order) -> device [pos_pad(M)][kBzCols]
@@ -421,6 +447,9 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
     p.tr_proj = (int32_t*)h->alloc("tr_proj", size_t(T) * B * 4);
     p.tr_obs = (int32_t*)h->alloc("tr_obs", size_t(T) * kEliteCost * 4);
     p.tr_cem = (int32_t*)h->alloc("tr_cem", size_t(T) * kElite * 4);
+    h->stage_bytes = stage_size(B, S, H, O, T);
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&h->stage), h->stage_bytes, hipHostMallocDefault));
+    HIPC(hipEventCreateWithFlags(&h->stage_ev, hipEventDisableTiming));
     upload(h, "basis", basis.data(), basis.size() * 4);
     upload(h, "guess_g", gg.data(), gg.size() * 8);
     upload(h, "proj_m", pm.data(), pm.size() * 8);
@@ -446,6 +475,8 @@ void mpcmmd_destroy(mpcmmd_handle* h) {
     (void)hipEventDestroy(pe.second.second);
   }
   for (auto e : h->free_events) (void)hipEventDestroy(e);
+  if (h->stage_ev) (void)hipEventDestroy(h->stage_ev);
+  if (h->stage) (void)hipHostFree(h->stage);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -474,6 +505,17 @@ int mpcmmd_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const flo
     check_device(h);
     Params& p = h->p;
     const int B = h->B, S = h->S, H = h->H, O = h->O, T = h->T;
+    if (h->stage_pending) HIPC(hipEventSynchronize(h->stage_ev));  // previous begin's copies done
+    h->stage_pending = false;
+    h->stage_used = 0;
+    // a failure after the first staged copy: drain them before the staging area is reused
+    struct DrainOnThrow {
+      mpcmmd_handle* h;
+      bool armed = true;
+      ~DrainOnThrow() {
+        if (armed) (void)hipStreamSynchronize(h->stream);
+      }
+    } drain{h};
     h->cost = cost_kind;
     p.cost = cost_kind;
     p.idx_mpc = idx_mpc;
@@ -492,17 +534,17 @@ int mpcmmd_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const flo
       for (int e = 0; e < 3; ++e) sc[2 * kNvar + k] += h->pc.proj_kinv_x[k * 14 + kNvar + e] * bx[e];
       for (int e = 0; e < 4; ++e) sc[3 * kNvar + k] += h->pc.proj_kinv_y[k * 15 + kNvar + e] * by[e];
     }
-    upload(h, "solve_c", sc.data(), sc.size() * 8);
+    upload_staged(h, "solve_c", sc.data(), sc.size() * 8);
     float st0[8] = {init_state[0], init_state[1], init_state[2], init_state[3],
                     atan2f(init_state[3], init_state[2]), 0.f, 0.f, 0.f};
-    upload(h, "st0", st0, sizeof(st0));
+    upload_staged(h, "st0", st0, sizeof(st0));
     std::vector<float> ob(size_t(2) * O * H);
     for (int o = 0; o < O; ++o)
       for (int t = 0; t < H; ++t) {
         ob[size_t(o) * H + t] = x_obs[o * kNum + t];
         ob[size_t(O) * H + o * H + t] = y_obs[o * kNum + t];
       }
-    upload(h, "obs", ob.data(), ob.size() * 4);
+    upload_staged(h, "obs", ob.data(), ob.size() * 4);
     // sampling_param (cem_helper.py:122-150): fixed key
     std::vector<float> z0;
     if (draws && draws->pop0) z0.assign(draws->pop0, draws->pop0 + size_t(B) * 8);
@@ -519,9 +561,9 @@ int mpcmmd_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const flo
         if (a < 4) v = fminf(fmaxf(v, 0.1f), 30.0f);
         pop[size_t(b) * 8 + a] = v;
       }
-    upload(h, "pop", pop.data(), pop.size() * 4);
-    upload(h, "mean", mean, 8 * 4);
-    upload(h, "cov", cov, 64 * 4);
+    upload_staged(h, "pop", pop.data(), pop.size() * 4);
+    upload_staged(h, "mean", mean, 8 * 4);
+    upload_staged(h, "cov", cov, 64 * 4);
     HIPC(hipMemsetAsync(p.lam_x, 0, size_t(B) * kNvar * 4, h->stream));
     HIPC(hipMemsetAsync(p.lam_y, 0, size_t(B) * kNvar * 4, h->stream));
     HIPC(hipMemsetAsync(p.s_lane, 0, size_t(B) * kLane * 4, h->stream));
@@ -535,9 +577,9 @@ int mpcmmd_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const flo
           for (int s = 0; s < S; ++s)
             for (int q = 0; q < H; ++q)
               r[((size_t(t) * 3 + k) * H + q) * S + s] = draws->roll[((size_t(t) * 3 + k) * S + s) * H + q];
-      upload(h, "roll", r.data(), r.size() * 4);
+      upload_staged(h, "roll", r.data(), r.size() * 4);
     }
-    if (h->ext_res) upload(h, "resample", draws->resample, size_t(T) * (B - kElite) * 8 * 4);
+    if (h->ext_res) upload_staged(h, "resample", draws->resample, size_t(T) * (B - kElite) * 8 * 4);
     if (cost_kind == MPCMMD_COST_MMD_OPT) {
       const size_t M1 = size_t(h->M) + 1;
       const bool ext_b = draws && (draws->beta_z0 || draws->beta_z);
@@ -551,6 +593,9 @@ int mpcmmd_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const flo
         gen_beta_tables(h);
       }
     }
+    HIPC(hipEventRecord(h->stage_ev, h->stream));
+    h->stage_pending = true;
+    drain.armed = false;
     h->begun = true;
     h->last_t = -1;
     return MPCMMD_OK;

@@ -72,10 +72,30 @@ def draws_philox(prob, acc, steer, noise, R, H, key, seed=0):
     return np.stack([ba, bs, nc])
 
 
+def draws_numpy(noise, acc, steer, R, H, key):
+    """The reference's own draws of compute_rollout_complete (:42-92):
+    ``np.random.seed(key)``, then NumPy multivariate_normal (gaussian) or
+    beta draws for acc and steer, then the const-noise normals -- as the
+    [3][R][H] array ``compute_stats`` / the GPU kernel take (for beta noise
+    rows 0 and 1 are the Beta samples themselves)."""
+    np.random.seed(key)
+    acc = np.asarray(acc, F64)[:H]
+    steer = np.asarray(steer, F64)[:H]
+    if noise == "gaussian":
+        na = np.random.multivariate_normal(np.zeros(H), np.eye(H), (R,))
+        ns = np.random.multivariate_normal(np.zeros(H), np.eye(H), (R,))
+    else:
+        na = np.random.beta(2 * np.abs(acc), 5 * np.abs(acc), (R, H))
+        ns = np.random.beta(2 * np.abs(steer) + 1e-5, 5 * np.abs(steer) + 1e-5, (R, H))
+    nc = np.random.multivariate_normal(np.zeros(H), np.eye(H), (R,))
+    return np.stack([na, ns, nc])
+
+
 def compute_stats(prob: Problem, cx, cy, init_state, x_obs_traj, y_obs_traj, noise, noise_level, acc_const,
-                  steer_const, draws):
+                  steer_const, draws, return_rollouts=False):
     """(count, count_lane) of one configuration (:134-171).  x_obs_traj,
-    y_obs_traj [O][100] fp32; draws [3][R][H]."""
+    y_obs_traj [O][100] fp32; draws [3][R][H].  With return_rollouts also
+    the [R][H] x / y rollouts (:148-149)."""
     H = prob.num_prime
     acc, steer = controls(prob, cx, cy)
     acc, steer = acc[:H], steer[:H]
@@ -116,4 +136,6 @@ def compute_stats(prob: Problem, cx, cy, init_state, x_obs_traj, y_obs_traj, noi
     lb = np.maximum(0.0, -yr + prob.y_lb)
     ub = np.maximum(0.0, yr - prob.y_ub)
     count_lane = int(np.max(np.count_nonzero(lb, axis=0)) + np.max(np.count_nonzero(ub, axis=0)))
+    if return_rollouts:
+        return count, count_lane, xr, yr
     return count, count_lane

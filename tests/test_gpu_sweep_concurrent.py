@@ -1,24 +1,28 @@
 """Concurrent sweep (optimizer.sweep.run_block_concurrent): configurations in
 flight on separate HIP streams give bit-identical rows to one-at-a-time
 solving through the drop-in CEM (the per-configuration RNG is keyed by its own
-idx_mpc), at the reference's num_batch = 100."""
+idx_mpc), at the reference's num_batch = 100.  Both scenario variants: the
+dynamic one changes y_lb / y_ub / K_steer on the device and feeds the
+library's QP obstacle tracks (synthetic_dynamic_obs/main_mpc.py:116-135)."""
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("variant", ["static", "dynamic"])
 @pytest.mark.parametrize("cost,n", [("cvar", 32), ("mmd_opt", 8)])
-def test_concurrent_equals_sequential(cost, n):
+def test_concurrent_equals_sequential(cost, n, variant):
     from optimizer import _native
     from optimizer.cem import CEM
     from optimizer.sweep import run_block, run_block_concurrent
-    prob = CEM(n, 4, 0.1, 20, "gaussian", 0.0, 0.0, num_batch=100, device=0)
-    init = np.array([0.0, 1.75, 5.0, 0.0, 0.0, 0.0], np.float32)
+    prob = CEM(n, 4, 0.1, 20, "gaussian", 0.0, 0.0, num_batch=100, device=0, variant=variant)
+    init = np.array([0.0, 1.75 if variant == "static" else -1.75, 5.0, 0.0, 0.0, 0.0], np.float32)
     mean = np.array([15.0] * 4 + [0.0] * 4, np.float32)
     cov = np.diag([20.0] * 4 + [100.0] * 4).astype(np.float32)
     ids = range(5)
-    seq = run_block(prob, cost, ids, init, mean, cov)
+    seq = run_block(prob, cost, ids, init, mean, cov, variant=variant)
     hs = [prob.handle] + [_native.Handle(prob._cfg) for _ in range(2)]
-    con = run_block_concurrent(prob, hs, cost, ids, init, mean, cov)
+    con = run_block_concurrent(prob, hs, cost, ids, init, mean, cov, variant=variant)
     assert np.array_equal(seq, con)
+    assert np.all(np.isfinite(seq[:, 1:25]))
