@@ -5,6 +5,7 @@
 //   k_mother    noisy control rows, n^2 mother rollouts (Cartesian product,
 //               cem_helper.py:469-530) with the ridge fit folded into the scan
 //               (compute_coeff, cem_helper.py:553-564) -> 22 features per row
+//   k_bdist     the M x M L1 distance matrix of the features (once)
 //   20 x { k_bsample  new samples of the beta-CEM (compute_beta.py:51-68)
 //          k_bselect  top-n |beta| rows and sigma per sample (compute_beta.py:41-49, 117-118)
 //          k_bkernel  Laplace-kernel row sums over the mother set and K_red
@@ -16,9 +17,12 @@
 //   k_mmdfinal  reduced-set rollouts, collision residual, MMD obs / lane
 //               (costs.py:121-135, 173-186)
 //
-// k_bselect and k_bqp are latency-bound chains and run as many single-wave
-// workgroups; the others use one workgroup per candidate (the candidate's beta-CEM
-// is sequential over its 20 iterations; candidates are independent).
+// The beta-iteration kernels work on a candidate range [p.b0, p.b0 + p.nb):
+// the host splits the batch into groups, each on its own stream, so the
+// kernels of different groups (bound by different units: MFMA, exp, fp64
+// FMA latency, LDS) run side by side.  Every supported size n <= 64
+// (M = n^2 <= 4096) takes the same kernels; the LDS-resident pieces are sized
+// at launch (ker_lds, elite_lds).
 //
 // The covariance of the beta-CEM is rank <= 10 plus 0.05 I
 // (jnp.cov of 11 elites, compute_beta.py:61).  Its Cholesky factor is never
@@ -55,6 +59,54 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 DEVI void wave_sync() {
   __builtin_amdgcn_wave_barrier();
   __asm__ volatile("" ::: "memory");
+}
+
+// ---- DPP helpers (gfx9 DPP controls) ------------------------------------
+// quad_perm(1,0,3,2) 0xB1, quad_perm(2,3,0,1) 0x4E, row_ror:4 0x124,
+// row_ror:8 0x128, row_bcast:15 0x142, row_bcast:31 0x143
+template <int CTRL, int ROWS = 0xF>
+DEVI int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, false);
+}
+template <int CTRL, int ROWS = 0xF>
+DEVI double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, int(b), CTRL, ROWS, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), CTRL, ROWS, 0xF, false);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+// sum of the 64 lanes, wave-uniform result (VALU only: quad / row butterflies,
+// then the row broadcasts into lane 63)
+DEVI int wave_total(int v) {
+  v += dpp_i<0xB1>(v);
+  v += dpp_i<0x4E>(v);
+  v += dpp_i<0x124>(v);
+  v += dpp_i<0x128>(v);
+  v += dpp_i<0x142, 0xA>(v);
+  v += dpp_i<0x143, 0xC>(v);
+  return __builtin_amdgcn_readlane(v, 63);
+}
+DEVI double readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane(int(b), l);
+  const int hi = __builtin_amdgcn_readlane(int(b >> 32), l);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+DEVI double wave_total(double v) {
+  v += dpp_d<0xB1>(v);
+  v += dpp_d<0x4E>(v);
+  v += dpp_d<0x124>(v);
+  v += dpp_d<0x128>(v);
+  v += dpp_d<0x142, 0xA>(v);
+  v += dpp_d<0x143, 0xC>(v);
+  return readlane_d(v, 63);
+}
+// sum over each row of 16 lanes (every lane of the row holds it)
+DEVI double row16_sum(double v) {
+  v += dpp_d<0xB1>(v);
+  v += dpp_d<0x4E>(v);
+  v += dpp_d<0x124>(v);
+  return v + dpp_d<0x128>(v);
 }
 
 // ------------------------------------------------------------------------
@@ -157,10 +209,12 @@ __global__ __launch_bounds__(kDistThreads) void k_bdist(Params p) {
 // top-n of |v_j| (j < M) in jnp.argsort order, one wave.  out[k] (k < n) are
 // the indices at sorted positions M-n+k (ascending by (|v|, j)).
 // Lane holds NQ keys (j = lane + 64 q).  The n-th largest key is found by
-// bisection on the key bits with ballot counts; the search stops as soon as
-// exactly n keys lie above the candidate threshold (continuous data: ~10 of
-// the 31 steps).  Ties at the threshold go to the largest indices.
-// scratch: 2 * 32 ints of LDS owned by the wave.
+// bisection on the key bits; the counts are VALU (per-lane compares, then a
+// DPP reduction of two samples' counts packed in 16-bit halves), so the
+// search does not serialise on the CU's scalar unit.  The search stops as
+// soon as exactly n keys lie above the candidate threshold (continuous data:
+// well before the 31 steps).  Ties at the threshold go to the largest
+// indices.  scratch: 2 * 64 ints of LDS owned by the wave.
 template <int NQ, class V>
 DEVI void load_keys(V val, int M, uint32_t* key) {
   const int lane = threadIdx.x & 63;
@@ -174,26 +228,41 @@ DEVI void load_keys(V val, int M, uint32_t* key) {
 
 // Threshold search for NB samples at once (independent chains interleave):
 // T[u] = the n-th largest key of sample u, or exact[u] when exactly n keys
-// are >= T[u] (the search stops early for continuous data).
+// are >= T[u].
 template <int NQ, int NB>
 DEVI void find_thresholds(const uint32_t (*key)[NQ], int nb, int n, uint32_t* T, bool* exact) {
+  constexpr int NP = (NB + 1) / 2;
 #pragma unroll
   for (int u = 0; u < NB; ++u) {
     T[u] = 0x80000000u;  // real keys have bit 31 set, padding keys are 0
     exact[u] = u >= nb;
   }
   for (int bit = 30; bit >= 0; --bit) {
-    bool all = true;
+    int packed[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) packed[i] = 0;
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
-      if (exact[u]) continue;
+      if (exact[u]) continue;  // wave-uniform
       const uint32_t cand = T[u] | (1u << bit);
-      int cnt = 0;
+      int c = 0;
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) cnt += __popcll(__ballot(key[u][q] >= cand));
-      if (cnt >= n) T[u] = cand;
-      exact[u] = cnt == n;
-      all = all && exact[u];
+      for (int q = 0; q < NQ; ++q) c += key[u][q] >= cand;
+      packed[u >> 1] += c << (16 * (u & 1));
+    }
+    bool all = true;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int tot = wave_total(packed[i]);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int u = 2 * i + h;
+        if (u >= NB || exact[u]) continue;
+        const int cnt = (tot >> (16 * h)) & 0xFFFF;
+        if (cnt >= n) T[u] |= 1u << bit;
+        exact[u] = cnt == n;
+        all = all && exact[u];
+      }
     }
     if (all) break;
   }
@@ -220,7 +289,7 @@ DEVI void emit_top(const uint32_t* key, uint32_t T, bool exact, int n, int32_t* 
   }
   const unsigned long long above = lane == 63 ? 0ull : (~0ull << (lane + 1));
   int* lj = scratch;
-  uint32_t* lk = reinterpret_cast<uint32_t*>(scratch + 32);
+  uint32_t* lk = reinterpret_cast<uint32_t*>(scratch + 64);
   int base = 0;
   int later_eq = 0;  // equal keys in q' > q
 #pragma unroll
@@ -256,7 +325,7 @@ DEVI void emit_top(const uint32_t* key, uint32_t T, bool exact, int n, int32_t* 
 // threshold searches interleave.  row(s) -> values, out(s) -> int32[n].
 template <int NQ, class Row, class Out>
 DEVI void select_batch(Row row, Out out, int first, int last, int stride, int M, int n, int* scratch) {
-  constexpr int NB = NQ <= 8 ? 4 : (NQ <= 12 ? 2 : 1);
+  constexpr int NB = NQ <= 8 ? 4 : (NQ <= 16 ? 2 : 1);
   for (int s0 = first; s0 < last; s0 += NB * stride) {
     uint32_t key[NB][NQ];
     const int nb = min(NB, (last - s0 + stride - 1) / stride);
@@ -269,33 +338,6 @@ DEVI void select_batch(Row row, Out out, int first, int last, int stride, int M,
 #pragma unroll
     for (int u = 0; u < NB; ++u)
       if (u < nb) emit_top<NQ>(key[u], T[u], exact[u], n, out(s0 + u * stride), scratch);
-  }
-}
-
-template <class Row, class Out>
-DEVI void select_rows(Row row, Out out, int first, int last, int stride, int M, int n, int* scratch) {
-  switch ((M + 63) >> 6) {
-#define MPCMMD_SEL_CASE(q) \
-  case q:                  \
-    return select_batch<q>(row, out, first, last, stride, M, n, scratch);
-    MPCMMD_SEL_CASE(1)
-    MPCMMD_SEL_CASE(2)
-    MPCMMD_SEL_CASE(3)
-    MPCMMD_SEL_CASE(4)
-    MPCMMD_SEL_CASE(5)
-    MPCMMD_SEL_CASE(6)
-    MPCMMD_SEL_CASE(7)
-    MPCMMD_SEL_CASE(8)
-    MPCMMD_SEL_CASE(9)
-    MPCMMD_SEL_CASE(10)
-    MPCMMD_SEL_CASE(11)
-    MPCMMD_SEL_CASE(12)
-    MPCMMD_SEL_CASE(13)
-    MPCMMD_SEL_CASE(14)
-    MPCMMD_SEL_CASE(15)
-#undef MPCMMD_SEL_CASE
-    default:
-      return select_batch<16>(row, out, first, last, stride, M, n, scratch);
   }
 }
 
@@ -402,7 +444,7 @@ DEVI void sample_block(const SampleBlock& cur, d4* S, float* Y, int p0, int M, i
 }
 
 __global__ __launch_bounds__(64 * kSampleWaves) void k_bsample(Params p, int tb) {
-  const int b = blockIdx.x, M = p.M, Pp = pos_pad(M);
+  const int b = p.b0 + blockIdx.x, M = p.M, Pp = pos_pad(M);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, h = lane >> 4;
   const int s0 = w * kTilesPerWave * 16;
@@ -437,13 +479,16 @@ __global__ __launch_bounds__(64 * kSampleWaves) void k_bsample(Params p, int tb)
 
 // ------------------------------------------------------------------------
 // k_bselect: top-n |beta| rows (compute_beta.py:117-118) and sigma of the
-// 100 samples.  Latency-bound per wave (ballot chains), so it runs as many
-// single-wave workgroups: wave (b, g) handles samples g, g+25, g+50, g+75.
+// 100 samples.  Latency-bound per wave, so it runs as many single-wave
+// workgroups: wave (b, g) handles samples g, g+25, g+50, g+75.
 constexpr int kSelGroups = 25;
 
+// NQ = keys per lane (M <= 64 NQ): one instantiation per size, so each has
+// its own register allocation
+template <int NQ>
 __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
-  __shared__ int scratch[64];
-  const int b = blockIdx.x, g = blockIdx.y, M = p.M, M1 = M + 1, n = p.n;
+  __shared__ int scratch[128];
+  const int b = p.b0 + blockIdx.x, g = blockIdx.y, M = p.M, M1 = M + 1, n = p.n;
   int32_t* sel = p.bsel + size_t(b) * kBetaSamples * n;
   float* sig = p.bsig + size_t(b) * kBetaSamples;
   const float* E = p.belite + (size_t(tb & 1) * p.B + b) * kBetaElite * M1;
@@ -460,7 +505,7 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
   // samples 0..10 of iteration tb >= 1 are the previous elites, whose rows
   // and sigma k_belite carried over
   const int s_lo = first_sample(tb);
-  select_rows(row, [&](int s) { return sel + s * n; }, s_lo + g, kBetaSamples, kSelGroups, M, n, scratch);
+  select_batch<NQ>(row, [&](int s) { return sel + s * n; }, s_lo + g, kBetaSamples, kSelGroups, M, n, scratch);
   const int s = s_lo + g + int(threadIdx.x) * kSelGroups;
   if (threadIdx.x < 4 && s < kBetaSamples) {
     const float v = row(s)(M);
@@ -471,10 +516,11 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
 // ------------------------------------------------------------------------
 // k_bkernel: one workgroup (1024 threads) per candidate.
 //
-//   rows     the distinct mother rows the samples selected (union, ~150 of
-//            484 on average); each is a row of the distance matrix k_bdist
+//   rows     the distinct mother rows the samples selected (union U, ~150 of
+//            484 at n = 22); each is a row of the distance matrix k_bdist
 //            wrote this outer iteration (kernel_computation.py:33-39), staged
-//            into LDS chunk by chunk with 16-byte loads
+//            into LDS by LDS-DMA, chunk c + 1 in flight while chunk c is
+//            summed (two buffers)
 //   pairs    (sample, reduced row) pairs sorted by row; an 8-lane group sums
 //            exp(-D[r][j] / sigma_s) over j (v_exp_f32 on d * (-log2 e /
 //            sigma), packed scale / add), and writes the sample's K_red
@@ -485,8 +531,8 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
 constexpr int kKerThreads = 1024;
 
 struct KerLds {
-  size_t sel, csg, cnt, start, fill, ulist, urank, pairs, pair_s, work, total;
-  int rows;  // D-chunk rows
+  size_t sel, csg, cnt, fill, start, ulist, urank, pairs, pair_s, work, total;
+  int rows;  // D rows per buffer (two buffers)
 };
 
 HDI KerLds ker_lds(int M, int n, size_t budget) {
@@ -497,34 +543,34 @@ HDI KerLds ker_lds(int M, int n, size_t budget) {
     o = (o + bytes + 15) & ~size_t(15);
     return at;
   };
-  L.sel = take(size_t(kBetaSamples) * n * 2);
+  L.sel = take(size_t(kBetaSamples) * n * 2);    // short
   L.csg = take(size_t(kBetaSamples) * 4);
-  L.cnt = take(size_t(M) * 4);
-  L.start = take(size_t(M) * 4);
+  L.cnt = take(size_t(M) * 4);                   // int (LDS atomics)
   L.fill = take(size_t(M) * 4);
-  L.ulist = take(size_t(M) * 4);
-  L.urank = take(size_t(M) * 4);
+  L.start = take(size_t(M) * 2);                 // ushort: <= 100 n
+  L.ulist = take(size_t(M) * 2);
+  L.urank = take(size_t(M) * 2);
   L.pairs = take(size_t(kBetaSamples) * n * 2);
   L.pair_s = take(size_t(kBetaSamples) * n);
   L.work = o;
   const size_t rest = budget > o ? budget - o : 0;
-  int rows = int(rest / (size_t(dist_stride(M)) * 4));
-  if (rows > 256) rows = 256;
+  int rows = int(rest / (size_t(2) * dist_stride(M) * 4));
+  if (rows > 128) rows = 128;
   L.rows = rows;
-  L.total = o + size_t(rows) * dist_stride(M) * 4;
+  L.total = o + size_t(2) * rows * dist_stride(M) * 4;
   return L;
 }
 
 constexpr size_t kLdsBudget = 160 * 1024 - 1024;
 // k_bkernel runs two workgroups per CU (one's D-row loads overlap the
-// other's exp sums) whenever half the LDS still holds this many D rows
+// other's exp sums) whenever half the LDS still holds this many D rows per buffer
 constexpr size_t kKerHalfBudget = 80 * 1024;
-constexpr int kKerMinRowsHalf = 8;
+constexpr int kKerMinRowsHalf = 4;
 constexpr float kNegLog2e = -1.44269504088896340736f;
 
 __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb, int budget) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int b = blockIdx.x, M = p.M, n = p.n, Md = dist_stride(M);
+  const int b = p.b0 + blockIdx.x, M = p.M, n = p.n, Md = dist_stride(M);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const KerLds C = ker_lds(M, n, size_t(budget));
@@ -532,10 +578,10 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb, int b
   float* csg = reinterpret_cast<float*>(smem + C.csg);
   double* rowsum = p.brow + size_t(b) * kBetaSamples * n;
   int* cnt = reinterpret_cast<int*>(smem + C.cnt);
-  int* start = reinterpret_cast<int*>(smem + C.start);
   int* fill = reinterpret_cast<int*>(smem + C.fill);
-  int* ulist = reinterpret_cast<int*>(smem + C.ulist);
-  int* urank = reinterpret_cast<int*>(smem + C.urank);
+  unsigned short* start = reinterpret_cast<unsigned short*>(smem + C.start);
+  unsigned short* ulist = reinterpret_cast<unsigned short*>(smem + C.ulist);
+  unsigned short* urank = reinterpret_cast<unsigned short*>(smem + C.urank);
   short* pairs = reinterpret_cast<short*>(smem + C.pairs);
   unsigned char* pair_s = reinterpret_cast<unsigned char*>(smem + C.pair_s);
   float* Dl = reinterpret_cast<float*>(smem + C.work);
@@ -571,9 +617,9 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb, int b
     x1 -= s1;
     x2 -= s2;
     for (int r = a; r < e; ++r) {
-      start[r] = x1;
-      urank[r] = x2;
-      if (cnt[r] > 0) ulist[x2] = r;
+      start[r] = (unsigned short)x1;
+      urank[r] = (unsigned short)x2;
+      if (cnt[r] > 0) ulist[x2] = (unsigned short)r;
       x1 += cnt[r];
       x2 += cnt[r] > 0;
     }
@@ -595,43 +641,52 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb, int b
   const int R = C.rows, q4 = Md >> 2;
   const int g = tid >> 3, gl = tid & 7, ng = kKerThreads >> 3;  // 8 lanes per pair
   const int ntri = n * (n - 1) / 2;
-  for (int c0 = 0; c0 < U; c0 += R) {
-    const int rc = min(R, U - c0);
-    __syncthreads();  // previous chunk consumed (and, first time, pairs built)
-    // LDS-DMA (global_load_lds_dwordx4): the chunk image is lane-linear (rows
-    // contiguous, no padding), each lane's source row is its own address
+  const int nchunk = (U + R - 1) / R;
+  // LDS-DMA (global_load_lds_dwordx4) of chunk c into buffer c & 1: the chunk
+  // image is lane-linear (rows contiguous, no padding), each lane's source
+  // row is its own address
+  auto issue = [&](int c) {
+    const int c0 = c * R, rc = min(R, U - c0);
+    float4* dst = reinterpret_cast<float4*>(Dl + size_t(c & 1) * R * Md);
     for (int idx = tid; idx < rc * q4; idx += kKerThreads) {
-      const int u = idx / q4, c = idx - u * q4;
-      __builtin_amdgcn_global_load_lds(Dg + size_t(ulist[c0 + u]) * q4 + c,
-                                       reinterpret_cast<float4*>(Dl) + (idx - (tid & 63)), 16, 0, 0);
+      const int u = idx / q4, cc = idx - u * q4;
+      __builtin_amdgcn_global_load_lds(Dg + size_t(ulist[c0 + u]) * q4 + cc, dst + (idx - (tid & 63)), 16, 0, 0);
     }
+  };
+  __syncthreads();  // pairs built
+  if (nchunk > 0) issue(0);
+  for (int c = 0; c < nchunk; ++c) {
+    // chunk c landed (each wave waits for its own DMA), every wave is done
+    // with chunk c - 1, whose buffer chunk c + 1 now reuses
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (c0 == 0) MPCMMD_STAMP(p, 18);
+    if (c + 1 < nchunk) issue(c + 1);
+    if (c == 0) MPCMMD_STAMP(p, 18);
+    const int c0 = c * R, rc = min(R, U - c0);
+    const float* Db = Dl + size_t(c & 1) * R * Md;
     const int p0 = start[ulist[c0]];
     const int p1 = start[ulist[c0 + rc - 1]] + cnt[ulist[c0 + rc - 1]];
-    const int J = Md >> 1;
+    const int nf4 = Md >> 5;  // float4s per lane of the 8-lane group
     for (int pi = p0 + g; pi < p1; pi += ng) {
       const int i = pairs[pi];
       const int s = pair_s[pi];
       const int k = i - s * n;
       const float cn = csg[s];
       const int u = urank[sl[i]] - c0;
-      const f2* drow = reinterpret_cast<const f2*>(Dl + size_t(u) * Md);
+      // lane gl reads float4s gl, gl + 8, ...: the group reads 128 contiguous bytes
+      const float4* drow = reinterpret_cast<const float4*>(Db + size_t(u) * Md) + gl;
       const f2 c2 = {cn, cn};
       f2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f};
-      int j = gl;
-      for (; j + 8 < J; j += 16) {
-        const f2 t0 = drow[j] * c2, t1 = drow[j + 8] * c2;
+#pragma unroll 4
+      for (int q = 0; q < nf4; ++q) {
+        const float4 d = drow[8 * q];
+        const f2 t0 = f2{d.x, d.y} * c2, t1 = f2{d.z, d.w} * c2;
         a0 += f2{__builtin_amdgcn_exp2f(t0.x), __builtin_amdgcn_exp2f(t0.y)};
         a1 += f2{__builtin_amdgcn_exp2f(t1.x), __builtin_amdgcn_exp2f(t1.y)};
       }
-      if (j < J) {
-        const f2 t0 = drow[j] * c2;
-        a0 += f2{__builtin_amdgcn_exp2f(t0.x), __builtin_amdgcn_exp2f(t0.y)};
-      }
       a0 += a1;
       // K_red[s][k][kk] for kk < k: row t_k of the distance matrix is in the chunk
-      const float* dr = Dl + size_t(u) * Md;
+      const float* dr = Db + size_t(u) * Md;
       float* kr = p.bkred + (size_t(b) * kBetaSamples + s) * ntri + k * (k - 1) / 2;
       for (int kk = gl; kk < k; kk += 8) kr[kk] = __builtin_amdgcn_exp2f(dr[sl[s * n + kk]] * cn);
       float a = a0.x + a0.y;
@@ -640,7 +695,7 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb, int b
       a += __shfl_xor(a, 4, 8);
       if (gl == 0) rowsum[i] = double(a);
     }
-    if (c0 == 0) MPCMMD_STAMP(p, 19);
+    if (c == 0) MPCMMD_STAMP(p, 19);
   }
   MPCMMD_STAMP(p, 20);
 }
@@ -658,13 +713,6 @@ __global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb, int b
 // broadcast of y_j) and a column sweep (backward, quad sum of partials).
 // Entries above the diagonal are kept at exactly 0, padding rows are
 // identity with zero right-hand sides.
-template <int CTRL>
-DEVI double dpp_d(double v) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, int(b), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), CTRL, 0xF, 0xF, false);
-  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
-}
 // value of quad lane l (0..3) in every lane of the quad; l is a constant
 // after unrolling, so the switch folds
 DEVI double quad_bcast(double v, int l) {
@@ -687,9 +735,9 @@ DEVI void bqp_quad(const Params& p, int tb) {
   const int n = p.n, M = p.M, q = threadIdx.x & 3;
   const int s_lo = first_sample(tb), per = kBetaSamples - s_lo;
   const int gq = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;
-  const bool ok = gq < p.B * per;
+  const bool ok = gq < p.nb * per;
   const int gqc = ok ? gq : 0;
-  const int b = gqc / per, s = s_lo + gqc % per;
+  const int b = p.b0 + gqc / per, s = s_lo + gqc % per;
   const int ntri = n * (n - 1) / 2;
   const float* kr = p.bkred + (size_t(b) * kBetaSamples + s) * ntri;
   const double* br = p.brow + (size_t(b) * kBetaSamples + s) * n;
@@ -824,7 +872,7 @@ DEVI void bqp_quad(const Params& p, int tb) {
   if (q == 0) p.bcost[size_t(b) * kBetaSamples + s] = float((c1 - delta * c2) - 2.0 * c3);
 }
 
-HDI int qp_np(int n) { return n <= 8 ? 8 : (n <= 16 ? 16 : (n <= 24 ? 24 : 32)); }
+HDI int qp_np(int n) { return n <= 8 ? 8 : (n <= 16 ? 16 : (n <= 24 ? 24 : (n <= 32 ? 32 : (n <= 48 ? 48 : 64)))); }
 constexpr int kQpThreads = 256;  // 64 QPs per workgroup
 
 template <int NP>
@@ -832,18 +880,103 @@ __global__ __launch_bounds__(kQpThreads) void k_bqp(Params p, int tb) {
   bqp_quad<NP>(p, tb);
 }
 
+// k_bqp_wave: the same QP for 32 < n <= 64, one wave per QP, lane i owns
+// row i of C (NP doubles in registers).  Right-looking Cholesky with the
+// column entries broadcast by v_readlane (entries above the diagonal are
+// left stale and zeroed when their column is reached, never read); forward
+// solves for g and 1 together; then, since C^-1 = L^-T L^-1,
+//   sum x1 = y2.y1, sum x2 = |y2|^2, beta = L^-T (y1 + alpha y2),
+// one backward solve (column sums as wave reductions).  The cost is
+// beta^T K beta - 2 g^T beta on the fp32-rounded beta with K_red re-read
+// (same value as the quad kernel's |L^T beta|^2 - delta |beta|^2 form).
+template <int NP>
+__global__ __launch_bounds__(256) void k_bqp_wave(Params p, int tb) {
+  const int lane = threadIdx.x & 63;
+  const int n = p.n, M = p.M;
+  const int s_lo = first_sample(tb), per = kBetaSamples - s_lo;
+  const int gq = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gq >= p.nb * per) return;  // whole waves
+  const int b = p.b0 + gq / per, s = s_lo + gq % per;
+  const int ntri = n * (n - 1) / 2;
+  const float* kr = p.bkred + (size_t(b) * kBetaSamples + s) * ntri;
+  const double* br = p.brow + (size_t(b) * kBetaSamples + s) * n;
+  const double inv_m = double(1.0f / float(M));
+  const double cdiag = double(1.0f + 0.05f);
+  const bool real = lane < n;
+  double A[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    double v = 0.0;
+    if (k < lane && real) v = double(kr[lane * (lane - 1) / 2 + k]);
+    if (k == lane) v = real ? cdiag : 1.0;
+    A[k] = v;
+  }
+  const double g = real ? br[lane] * inv_m : 0.0;
+  double rdiag = 1.0;
+  // Cholesky, column j
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const double djj = readlane_d(A[j], j);
+    double y = __builtin_amdgcn_rsq(djj);  // 1/sqrt: v_rsq_f64 + two Newton steps
+    y = y * fma(-0.5 * djj, y * y, 1.5);
+    y = y * fma(-0.5 * djj, y * y, 1.5);
+    const double lij = A[j] * y;
+    A[j] = lane > j ? lij : (lane == j ? djj * y : 0.0);
+    if (lane == j) rdiag = y;
+#pragma unroll
+    for (int k = j + 1; k < NP; ++k) A[k] = fma(-A[j], readlane_d(A[j], k), A[k]);
+  }
+  // forward: L y = (g, 1)
+  double y1 = g, y2 = real ? 1.0 : 0.0;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const double t1 = readlane_d(y1 * rdiag, j), t2 = readlane_d(y2 * rdiag, j);
+    y1 = lane == j ? t1 : fma(-A[j], t1, y1);
+    y2 = lane == j ? t2 : fma(-A[j], t2, y2);
+  }
+  const double s1 = wave_total(y2 * y1), s2 = wave_total(y2 * y2);
+  const double alpha = (1.0 - s1) / s2;
+  const double wv = fma(alpha, y2, y1);
+  // backward: L^T beta = w
+  double bet = 0.0;
+#pragma unroll
+  for (int j = NP - 1; j >= 0; --j) {
+    const double r = wave_total(A[j] * bet);
+    if (lane == j) bet = (wv - r) * rdiag;
+  }
+  const float bf = real ? float(bet) : 0.0f;
+  const double bd = double(bf);
+  // cost = bd^T K bd - 2 g^T bd, K = K_red (unit diagonal)
+  double kb = bd;
+#pragma unroll 8
+  for (int k = 0; k < NP; ++k) {
+    const double bk = readlane_d(bd, k);
+    if (k != lane && real && k < n) {
+      const int e = k < lane ? lane * (lane - 1) / 2 + k : k * (k - 1) / 2 + lane;
+      kb = fma(double(kr[e]), bk, kb);
+    }
+  }
+  const double c1 = wave_total(bd * kb), c3 = wave_total(g * bd);
+  float* bt = p.btop + (size_t(b) * kBetaSamples + s) * n;
+  if (real) bt[lane] = bf;
+  if (lane == 0) p.bcost[size_t(b) * kBetaSamples + s] = float(c1 - 2.0 * c3);
+}
+
 // ------------------------------------------------------------------------
 // k_belite: elites, mean, next generators; on the last iteration the outputs
 // (beta_best, sigma_best with the post-update quirk Q4, the reduced set).
+// Positions are thread-strided (lane = position), so a wave covers four
+// whole 16-position blocks: mean and u_j stay in the thread's registers and
+// the block sums of u u^T are row-of-16 DPP reductions.  LDS holds only the
+// block sums (nblk x 66 fp64) and small bookkeeping.
 struct EliteLds {
-  size_t U, Gb, misc, carry, total;
+  size_t Gb, misc, carry, total;
 };
 HDI EliteLds elite_lds(int M1) {
   EliteLds L{};
   const int nblk = (M1 + 15) / 16;
-  L.U = 0;
-  L.Gb = (size_t(M1) * 11 * 8 + 15) & ~size_t(15);
-  L.misc = L.Gb + ((size_t(nblk) * 66 * 8 + 15) & ~size_t(15));
+  L.Gb = 0;
+  L.misc = (size_t(nblk) * 66 * 8 + 15) & ~size_t(15);
   L.carry = L.misc + 1024;
   L.total = L.carry + size_t(kBetaElite) * (2 * kMaxReduced + 2) * 4;
   return L;
@@ -854,13 +987,13 @@ HDI int sym11(int a, int c) { return a * 11 - a * (a - 1) / 2 + (c - a); }
 
 __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int b = blockIdx.x, M = p.M, M1 = M + 1, n = p.n, tid = threadIdx.x;
+  const int b = p.b0 + blockIdx.x, M = p.M, M1 = M + 1, n = p.n, tid = threadIdx.x;
   const EliteLds C = elite_lds(M1);
-  double* Ul = reinterpret_cast<double*>(smem + C.U);
   double* Gb = reinterpret_cast<double*>(smem + C.Gb);
   int* elite = reinterpret_cast<int*>(smem + C.misc);    // [11]
   int* info = elite + 16;                                 // [0] imin, [1] any NaN
   float* cst = reinterpret_cast<float*>(info + 16);       // [100]
+  float* sig_new = cst + kBetaSamples;                    // [11] sigma of the new elite rows
   const float* costs = p.bcost + size_t(b) * kBetaSamples;
   if (tid < kBetaSamples) cst[tid] = costs[tid];
   if (tid == 0) {
@@ -912,63 +1045,64 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
       p.bcost[rb + tid] = ccost[tid];
     }
   }
-  // ---- E_new = the 11 elite sample vectors (rows 0..10 of the next samples):
-  // previous elites, this iteration's new samples (ygen), or at tb = 0 the
-  // initial samples
+  // ---- per position j: E_new column (the 11 elite sample values: previous
+  // elites, this iteration's new samples (ygen) or, at tb = 0, the initial
+  // samples), mean, u = (E - mean) / sqrt(10), block sums of u u^T
   const float* Eold = p.belite + (size_t(tb & 1) * p.B + b) * kBetaElite * M1;
   float* Enew = p.belite + (size_t((tb + 1) & 1) * p.B + b) * kBetaElite * M1;
   const int ys = ygen_stride(M);
   const float* Y = p.ygen + size_t(b) * kBzCols * ys;
-  for (int i = tid; i < kBetaElite * M1; i += blockDim.x) {
-    const int q = i / M1, j = i - q * M1;
-    const int e = elite[q];
-    float v;
-    if (tb == 0) {
-      v = float(kSqrt20 * double(p.beta_z0[size_t(e) * M1 + j]));
-      if (j == M) v = fmaxf(v, 0.01f);
-    } else if (e < kBetaElite) {
-      v = Eold[size_t(e) * M1 + j];
-    } else {
-      v = Y[size_t(e - kBetaElite) * ys + j];
-    }
-    Enew[i] = v;
-  }
-  __syncthreads();
-  // ---- outputs of the beta-CEM on its last iteration (compute_beta.py:152-157)
-  const bool last = tb == kBetaIters - 1;
-  // ---- mean, U = (E - mean) / sqrt(10), generators of the next iteration
   const double rs10 = 1.0 / sqrt(10.0);
   double* gen = p.gen + size_t(b) * pos_pad(M) * kGenStride;
-  for (int j = tid; j < M1; j += blockDim.x) {
-    double s = 0.0;
-    for (int q = 0; q < kBetaElite; ++q) s = s + double(Enew[size_t(q) * M1 + j]);
-    const double m = s / double(kBetaElite);
-    double* gj = gen + size_t(j) * kGenStride + kGenU;
-    for (int q = 0; q < kBetaElite; ++q) {
-      const double u = (double(Enew[size_t(q) * M1 + j]) - m) * rs10;
-      Ul[j * 11 + q] = u;
-      gj[q] = u;
-    }
-    p.genm[size_t(b) * pos_pad(M) + j] = double(float(m));
-  }
-  __syncthreads();
-  // level 1: block sums of u u^T over 16 positions (66 packed entries)
   const int nblk = (M1 + 15) / 16;
-  for (int i = tid; i < nblk * 66; i += blockDim.x) {
-    const int blk = i / 66, e = i - blk * 66;
-    int a = 0, c = e;
-    while (c >= 11 - a) {
-      c -= 11 - a;
-      ++a;
+  const int span = ((nblk * 16 + 63) / 64) * 64;  // whole waves
+  for (int j = tid; j < span; j += blockDim.x) {
+    const bool valid = j < M1;
+    double u[kBetaElite];
+    {
+      float v[kBetaElite];
+      double s = 0.0;
+#pragma unroll
+      for (int q = 0; q < kBetaElite; ++q) {
+        const int e = elite[q];
+        float x = 0.0f;
+        if (valid) {
+          if (tb == 0) {
+            x = float(kSqrt20 * double(p.beta_z0[size_t(e) * M1 + j]));
+            if (j == M) x = fmaxf(x, 0.01f);
+          } else if (e < kBetaElite) {
+            x = Eold[size_t(e) * M1 + j];
+          } else {
+            x = Y[size_t(e - kBetaElite) * ys + j];
+          }
+          Enew[size_t(q) * M1 + j] = x;
+          if (j == M) sig_new[q] = x;
+        }
+        v[q] = x;
+        s = s + double(x);
+      }
+      const double m = s / double(kBetaElite);
+#pragma unroll
+      for (int q = 0; q < kBetaElite; ++q) u[q] = valid ? (double(v[q]) - m) * rs10 : 0.0;
+      if (valid) {
+        double* gj = gen + size_t(j) * kGenStride + kGenU;
+#pragma unroll
+        for (int q = 0; q < kBetaElite; ++q) gj[q] = u[q];
+        p.genm[size_t(b) * pos_pad(M) + j] = double(float(m));
+      }
     }
-    c += a;
-    double s = 0.0;
-    const int k1 = min(M1, blk * 16 + 16);
-    for (int k = blk * 16; k < k1; ++k) s += Ul[k * 11 + a] * Ul[k * 11 + c];
-    Gb[i] = s;
+    // level 1: block sums of u u^T over 16 positions (66 packed entries)
+    const int blk = j >> 4;
+#pragma unroll
+    for (int a = 0; a < 11; ++a)
+#pragma unroll
+      for (int c = a; c < 11; ++c) {
+        const double t = row16_sum(u[a] * u[c]);
+        if ((j & 15) == 0 && blk < nblk) Gb[blk * 66 + sym11(a, c)] = t;
+      }
   }
   __syncthreads();
-  // block prefix: Gb[blk] <- Phi at the start of blk = I + sum_{<blk} / d
+  // block prefix: phib[blk] <- Phi at the start of blk = I + sum_{<blk} / d
   if (tid < 66) {
     int a = 0, c = tid;
     while (c >= 11 - a) {
@@ -986,7 +1120,7 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
   }
   // last iteration: beta_best / reduced set of argmin (pre-update) and, when
   // argmin is a carried elite, sigma_best (Q4); k_bsigma handles a new sample
-  if (last) {
+  if (tb == kBetaIters - 1) {
     const int* bsel = p.bsel + (size_t(b) * kBetaSamples + imin) * n;
     for (int i = tid; i < n; i += blockDim.x) {
       p.bestsel[size_t(b) * n + i] = bsel[i];
@@ -994,7 +1128,7 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
     }
     if (tid == 0) {
       p.bimin[b] = imin;
-      if (imin < kBetaElite) p.sigma[b] = Enew[size_t(imin) * M1 + M];
+      if (imin < kBetaElite) p.sigma[b] = sig_new[imin];
     }
   }
 }
@@ -1007,7 +1141,7 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
 // this phase's register count (184 VGPRs).
 __global__ __launch_bounds__(64) void k_bgen(Params p) {
   __shared__ double us[64 * 11];  // u of this workgroup's 64 positions (whole 16-blocks)
-  const int b = blockIdx.y, M = p.M, M1 = M + 1;
+  const int b = p.b0 + blockIdx.y, M = p.M, M1 = M + 1;
   const int j0 = blockIdx.x * 64, j = j0 + threadIdx.x;
   const int nblk = (M1 + 15) / 16;
   double* gen = p.gen + size_t(b) * pos_pad(M) * kGenStride;
@@ -1088,7 +1222,7 @@ __global__ __launch_bounds__(64) void k_bgen(Params p) {
 // compute_beta.py:133-145): y_M = mean_M + L_MM z_M + u_M . sum_{j<M} w_j z_j
 __global__ __launch_bounds__(kThreads) void k_bsigma(Params p, int tb) {
   __shared__ double red[(kThreads / 64) * 11];
-  const int b = blockIdx.x, M = p.M, tid = threadIdx.x;
+  const int b = p.b0 + blockIdx.x, M = p.M, tid = threadIdx.x;
   const int imin = p.bimin[b];
   if (imin < kBetaElite) return;  // k_belite wrote it
   const double* gen = p.gen + size_t(b) * pos_pad(M) * kGenStride;
@@ -1178,12 +1312,12 @@ __global__ __launch_bounds__(64) void k_mmdfinal(Params p, int t) {
 bool mmdopt_supported(int n, int H, int O, std::string* why) {
   const int M = n * n;
   if (n > kMaxReduced) {
-    if (why) *why = "mmd_opt needs num_reduced <= 32";
+    if (why) *why = "mmd_opt needs num_reduced <= 64";
     return false;
   }
   const KerLds k = ker_lds(M, n, kLdsBudget);
   if (k.rows < 1 || k.total > kLdsBudget) {
-    if (why) *why = "mmd_opt: num_reduced^2 too large for the LDS-resident kernel-sum stage";
+    if (why) *why = "mmd_opt: num_reduced^2 too large for the LDS-staged kernel-sum stage";
     return false;
   }
   const EliteLds e = elite_lds(M + 1);
@@ -1206,16 +1340,51 @@ void launch_bdist(const Params& p, hipStream_t s) {
 }
 
 void launch_bsample(const Params& p, int tb, hipStream_t s) {
-  hipLaunchKernelGGL(k_bsample, dim3(p.B), dim3(64 * kSampleWaves), 0, s, p, tb);
+  hipLaunchKernelGGL(k_bsample, dim3(p.nb), dim3(64 * kSampleWaves), 0, s, p, tb);
+}
+
+template <int NQ>
+void launch_bselect_q(const Params& p, int tb, hipStream_t s) {
+  hipLaunchKernelGGL(k_bselect<NQ>, dim3(p.nb, kSelGroups), dim3(64), 0, s, p, tb);
 }
 
 void launch_bselect(const Params& p, int tb, hipStream_t s) {
-  hipLaunchKernelGGL(k_bselect, dim3(p.B, kSelGroups), dim3(64), 0, s, p, tb);
+  const int nq = (p.M + 63) >> 6;
+  switch (nq) {
+#define MPCMMD_SEL_CASE(q) \
+  case q:                  \
+    return launch_bselect_q<q>(p, tb, s);
+    MPCMMD_SEL_CASE(1)
+    MPCMMD_SEL_CASE(2)
+    MPCMMD_SEL_CASE(3)
+    MPCMMD_SEL_CASE(4)
+    MPCMMD_SEL_CASE(5)
+    MPCMMD_SEL_CASE(6)
+    MPCMMD_SEL_CASE(7)
+    MPCMMD_SEL_CASE(8)
+    MPCMMD_SEL_CASE(9)
+    MPCMMD_SEL_CASE(10)
+    MPCMMD_SEL_CASE(11)
+    MPCMMD_SEL_CASE(12)
+    MPCMMD_SEL_CASE(13)
+    MPCMMD_SEL_CASE(14)
+    MPCMMD_SEL_CASE(15)
+    MPCMMD_SEL_CASE(16)
+#undef MPCMMD_SEL_CASE
+    default:
+      break;
+  }
+  if (nq <= 24) return launch_bselect_q<24>(p, tb, s);
+  if (nq <= 32) return launch_bselect_q<32>(p, tb, s);
+  if (nq <= 40) return launch_bselect_q<40>(p, tb, s);
+  if (nq <= 48) return launch_bselect_q<48>(p, tb, s);
+  return launch_bselect_q<64>(p, tb, s);
 }
 
 void launch_bqp(const Params& p, int tb, hipStream_t s) {
-  const int qps = p.B * (kBetaSamples - first_sample(tb));
+  const int qps = p.nb * (kBetaSamples - first_sample(tb));
   const dim3 grid((qps * 4 + kQpThreads - 1) / kQpThreads);
+  const dim3 grid_wave((qps + 3) / 4);
   switch (qp_np(p.n)) {
     case 8:
       hipLaunchKernelGGL((k_bqp<8>), grid, dim3(kQpThreads), 0, s, p, tb);
@@ -1226,8 +1395,14 @@ void launch_bqp(const Params& p, int tb, hipStream_t s) {
     case 24:
       hipLaunchKernelGGL((k_bqp<24>), grid, dim3(kQpThreads), 0, s, p, tb);
       return;
-    default:
+    case 32:
       hipLaunchKernelGGL((k_bqp<32>), grid, dim3(kQpThreads), 0, s, p, tb);
+      return;
+    case 48:
+      hipLaunchKernelGGL((k_bqp_wave<48>), grid_wave, dim3(256), 0, s, p, tb);
+      return;
+    default:
+      hipLaunchKernelGGL((k_bqp_wave<64>), grid_wave, dim3(256), 0, s, p, tb);
       return;
   }
 }
@@ -1236,14 +1411,14 @@ void launch_bkernel(const Params& p, int tb, hipStream_t s) {
   size_t budget = kKerHalfBudget;
   if (ker_lds(p.M, p.n, budget).rows < kKerMinRowsHalf) budget = kLdsBudget;
   const KerLds k = ker_lds(p.M, p.n, budget);
-  hipLaunchKernelGGL(k_bkernel, dim3(p.B), dim3(kKerThreads), k.total, s, p, tb, int(budget));
+  hipLaunchKernelGGL(k_bkernel, dim3(p.nb), dim3(kKerThreads), k.total, s, p, tb, int(budget));
 }
 
 void launch_belite(const Params& p, int tb, hipStream_t s) {
   const EliteLds e = elite_lds(p.M + 1);
-  hipLaunchKernelGGL(k_belite, dim3(p.B), dim3(kThreads), e.total, s, p, tb);
-  hipLaunchKernelGGL(k_bgen, dim3((p.M + 1 + 63) / 64, p.B), dim3(64), 0, s, p);
-  if (tb == kBetaIters - 1) hipLaunchKernelGGL(k_bsigma, dim3(p.B), dim3(kThreads), 0, s, p, tb);
+  hipLaunchKernelGGL(k_belite, dim3(p.nb), dim3(kThreads), e.total, s, p, tb);
+  hipLaunchKernelGGL(k_bgen, dim3((p.M + 1 + 63) / 64, p.nb), dim3(64), 0, s, p);
+  if (tb == kBetaIters - 1) hipLaunchKernelGGL(k_bsigma, dim3(p.nb), dim3(kThreads), 0, s, p, tb);
 }
 
 void launch_mmdfinal(const Params& p, int t, hipStream_t s) {

@@ -11,7 +11,7 @@
 namespace mpcmmd {
 
 constexpr int kMaxH = 100;
-constexpr int kMaxReduced = 32;        // n for mmd_opt (M = n^2 <= 1024) -- see DESIGN.md
+constexpr int kMaxReduced = 64;        // n for mmd_opt (M = n^2 <= 4096) -- see DESIGN.md
 constexpr int kBetaSamples = 100;      // compute_beta.py:14
 constexpr int kBetaIters = 20;         // compute_beta.py:15
 constexpr int kBetaElite = 11;         // compute_beta.py:26
@@ -30,8 +30,9 @@ HDI_CONST int ygen_stride(int M) { return ((M + 1) + 31) & ~31; }
 // kBzCols samples
 constexpr int kBzCols = 96;
 HDI_CONST int pos_pad(int M) { return ((M + 1) + 31) & ~31; }  // whole pairs of 16-blocks
-// row stride (floats) of the mother distance matrix; pad columns hold +inf
-HDI_CONST int dist_stride(int M) { return (M + 3) & ~3; }
+// row stride (floats) of the mother distance matrix: whole float4s for each
+// lane of an 8-lane group (k_bkernel); pad columns hold +inf
+HDI_CONST int dist_stride(int M) { return (M + 31) & ~31; }
 
 struct Params {
   // shapes / configuration
@@ -40,6 +41,9 @@ struct Params {
   int32_t noise;     // MPCMMD_NOISE_*
   int32_t idx_mpc;
   uint32_t seed;
+  // candidate range of one beta-CEM launch: [b0, b0 + nb) (the beta-iteration
+  // kernels run per candidate group, each group on its own stream)
+  int32_t b0, nb;
   float sigma_acc, sigma_steer, acc_const, steer_const, K_steer;
   float y_lb, y_ub, v_des;
   float w_obs, w_lane;

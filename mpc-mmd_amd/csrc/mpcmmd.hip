@@ -7,7 +7,9 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -87,6 +89,12 @@ struct mpcmmd_handle {
   size_t stage_bytes = 0, stage_used = 0;
   hipEvent_t stage_ev = nullptr;
   bool stage_pending = false;
+  // candidate groups of the beta-CEM, each on its own stream (kernels of
+  // different groups overlap); 1 = everything on the handle's stream
+  static constexpr int kMaxGroups = 4;
+  int groups = 1;
+  hipStream_t gstream[kMaxGroups] = {};
+  hipEvent_t gev_start = nullptr, gev_done[kMaxGroups] = {};
   // profiling
   bool prof = false;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -222,14 +230,40 @@ void gen_beta_tables(mpcmmd_handle* h) {
   h->beta_tables_internal = true;
 }
 
-// one beta-CEM iteration (compute_beta.py:112-147)
-void run_beta_iteration(mpcmmd_handle* h, int tb) {
-  const Params& p = h->p;
-  if (tb > 0) h->launch(kKBSample, [&] { launch_bsample(p, tb, h->stream); });
-  h->launch(kKBSelect, [&] { launch_bselect(p, tb, h->stream); });
-  h->launch(kKBKernel, [&] { launch_bkernel(p, tb, h->stream); });
-  h->launch(kKBQp, [&] { launch_bqp(p, tb, h->stream); });
-  h->launch(kKBElite, [&] { launch_belite(p, tb, h->stream); });
+// one beta-CEM iteration (compute_beta.py:112-147) of candidates [p.b0, p.b0 + p.nb)
+void run_beta_iteration(mpcmmd_handle* h, const Params& p, int tb, hipStream_t st) {
+  if (tb > 0) h->launch(kKBSample, [&] { launch_bsample(p, tb, st); });
+  h->launch(kKBSelect, [&] { launch_bselect(p, tb, st); });
+  h->launch(kKBKernel, [&] { launch_bkernel(p, tb, st); });
+  h->launch(kKBQp, [&] { launch_bqp(p, tb, st); });
+  h->launch(kKBElite, [&] { launch_belite(p, tb, st); });
+}
+
+// the 20 beta-CEM iterations of every candidate: one chain per candidate
+// group, each group on its own stream between two events of the handle's
+// stream (profiling runs them on the handle's stream, one after another,
+// so the HIP-event timings are per kernel)
+void run_beta_cem(mpcmmd_handle* h) {
+  const int B = h->B, G = h->prof ? 1 : h->groups;
+  if (G <= 1) {
+    for (int tb = 0; tb < kBetaIters; ++tb) run_beta_iteration(h, h->p, tb, h->stream);
+    return;
+  }
+  std::vector<Params> pg(G, h->p);
+  const int per = (B + G - 1) / G;
+  for (int g = 0; g < G; ++g) {
+    pg[g].b0 = g * per;
+    pg[g].nb = std::max(0, std::min(per, B - g * per));
+  }
+  HIPC(hipEventRecord(h->gev_start, h->stream));
+  for (int g = 0; g < G; ++g) HIPC(hipStreamWaitEvent(h->gstream[g], h->gev_start, 0));
+  for (int tb = 0; tb < kBetaIters; ++tb)
+    for (int g = 0; g < G; ++g)
+      if (pg[g].nb > 0) run_beta_iteration(h, pg[g], tb, h->gstream[g]);
+  for (int g = 0; g < G; ++g) {
+    HIPC(hipEventRecord(h->gev_done[g], h->gstream[g]));
+    HIPC(hipStreamWaitEvent(h->stream, h->gev_done[g], 0));
+  }
 }
 
 void run_stage(mpcmmd_handle* h, int stage, int t) {
@@ -247,7 +281,7 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
         if (!h->mmd_ok) throw std::invalid_argument("mmd_opt unsupported for this configuration: " + h->mmd_why);
         h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
         h->launch(kKBDist, [&] { launch_bdist(p, h->stream); });
-        for (int tb = 0; tb < kBetaIters; ++tb) run_beta_iteration(h, tb);
+        run_beta_cem(h);
         h->launch(kKMmdFinal, [&] { launch_mmdfinal(p, t, h->stream); });
       } else {
         if (p.noise == MPCMMD_NOISE_BETA) h->launch(kKBetaPlanes, [&] { launch_beta_planes(p, t, h->stream); });
@@ -353,6 +387,8 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
     p.T = T;
     p.noise = c.noise;
     p.seed = c.seed;
+    p.b0 = 0;
+    p.nb = B;
     p.sigma_acc = c.noise_level;
     p.sigma_steer = c.noise_level;
     p.acc_const = c.acc_const_noise;
@@ -447,6 +483,14 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
     p.tr_proj = (int32_t*)h->alloc("tr_proj", size_t(T) * B * 4);
     p.tr_obs = (int32_t*)h->alloc("tr_obs", size_t(T) * kEliteCost * 4);
     p.tr_cem = (int32_t*)h->alloc("tr_cem", size_t(T) * kElite * 4);
+    if (const char* g = std::getenv("MPCMMD_GROUPS")) h->groups = std::max(1, std::min(mpcmmd_handle::kMaxGroups, std::atoi(g)));
+    if (h->groups > 1) {
+      HIPC(hipEventCreateWithFlags(&h->gev_start, hipEventDisableTiming));
+      for (int g = 0; g < h->groups; ++g) {
+        HIPC(hipStreamCreateWithFlags(&h->gstream[g], hipStreamNonBlocking));
+        HIPC(hipEventCreateWithFlags(&h->gev_done[g], hipEventDisableTiming));
+      }
+    }
     h->stage_bytes = stage_size(B, S, H, O, T);
     HIPC(hipHostMalloc(reinterpret_cast<void**>(&h->stage), h->stage_bytes, hipHostMallocDefault));
     HIPC(hipEventCreateWithFlags(&h->stage_ev, hipEventDisableTiming));
@@ -476,6 +520,12 @@ void mpcmmd_destroy(mpcmmd_handle* h) {
   }
   for (auto e : h->free_events) (void)hipEventDestroy(e);
   if (h->stage_ev) (void)hipEventDestroy(h->stage_ev);
+  for (int g = 0; g < mpcmmd_handle::kMaxGroups; ++g) {
+    if (h->gstream[g]) (void)hipStreamSynchronize(h->gstream[g]);
+    if (h->gstream[g]) (void)hipStreamDestroy(h->gstream[g]);
+    if (h->gev_done[g]) (void)hipEventDestroy(h->gev_done[g]);
+  }
+  if (h->gev_start) (void)hipEventDestroy(h->gev_start);
   if (h->stage) (void)hipHostFree(h->stage);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;

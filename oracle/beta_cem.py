@@ -40,15 +40,26 @@ def select_top(samples, M, n):
     return np.argsort(keys, axis=1, kind="stable")[:, M - n:]
 
 
-def reduced_qp(prob, F, top, sigma, M):
+def distance_matrix(F):
+    """All L1 distances of the mother features [M, M] (the rows
+    ``reduced_qp`` gathers; bit-identical to computing them per sample)."""
+    return l1_dist(F[:, None, :], F[None, :, :])
+
+
+def reduced_qp(prob, F, top, sigma, M, D=None):
     """Kernels (compute_beta.py:120-127, kernel_computation.py:19-65) and the
     equality-constrained QP ``compute_beta_reduced`` (compute_beta.py:70-91)
     for every sample.  Returns beta_top [K, n] fp32, cost [K] fp32,
-    K_red [K, n, n] fp32, rowsum [K, n] fp64."""
+    K_red [K, n, n] fp32, rowsum [K, n] fp64.  ``D``: the precomputed
+    ``distance_matrix(F)`` (large M: gathered instead of recomputed)."""
     K, n = top.shape
-    A = F[top]                                            # [K, n, 22]
-    D_red = l1_dist(A[:, :, None, :], A[:, None, :, :])    # [K, n, n]
-    D_mix = l1_dist(A[:, :, None, :], F[None, None, :, :])  # [K, n, M]
+    if D is None:
+        A = F[top]                                            # [K, n, 22]
+        D_red = l1_dist(A[:, :, None, :], A[:, None, :, :])    # [K, n, n]
+        D_mix = l1_dist(A[:, :, None, :], F[None, None, :, :])  # [K, n, M]
+    else:
+        D_mix = D[top]                                         # [K, n, M]
+        D_red = np.take_along_axis(D_mix, top[:, None, :], axis=2)
     sig = sigma.astype(F32)[:, None, None]
     K_red = np.exp((-D_red) / sig).astype(F32)
     K_mix = np.exp((-D_mix) / sig).astype(F32)
@@ -87,10 +98,11 @@ def compute_cem(prob, cx_m, cy_m, z0, z, trace=None):
     samples[:, M] = np.maximum(samples[:, M], F32(prob.sigma_clip))
     res = np.zeros(T, F32)
     out = None
+    Dm = distance_matrix(F) if M > 256 else None
     for t in range(T):
         sigma = samples[:, M].copy()
         top = select_top(samples, M, n)
-        beta, cost, K_red, _ = reduced_qp(prob, F, top, sigma, M)
+        beta, cost, K_red, _ = reduced_qp(prob, F, top, sigma, M, Dm)
         # compute_mean_cov_beta (:51-68)
         idx_e = argsort_stable(cost)[:E]
         El = samples[idx_e].astype(F64)

@@ -78,3 +78,42 @@ def make_pair(native, cost, noise="gaussian", n=16, O=3, H=10, B=32, T=3, level=
     x, y, vx, vy, psi = scenario(O, seed)
     xo, yo, _ = compute_obs_trajectories(ora.prob, x, y, vx, vy, psi)
     return ora, nat, xo, yo
+
+
+def beta_cem_trace(ora, st, acc, steer, draws, t):
+    """The oracle's beta-CEM of ONE candidate (controls acc, steer [100]) at
+    outer iteration t, with its per-iteration trace (costs, elites)."""
+    from oracle import beta_cem as bc
+    from oracle import helper as Hh
+    p = ora.prob
+    H = p.num_prime
+    acc_n, steer_n = Hh.noisy_controls(p, acc[None, :H], steer[None, :H], draws, t, p.num_reduced)
+    acc_m, steer_m = Hh.mother_controls(acc_n, steer_n)
+    xm, ym = Hh.rollout(p, acc_m, steer_m, st["st0"])
+    cxm, cym = Hh.compute_coeff(p, xm, ym)
+    trace = []
+    beta, res, sigma, sel = bc.compute_cem(p, cxm[0], cym[0], draws.beta_z0, draws.beta_z, trace)
+    return dict(beta=beta, res=res, sigma=sigma, sel=sel, trace=trace)
+
+
+def beta_near_tie(tr, res_gpu, tol=1e-5):
+    """Explain a beta-CEM divergence between GPU and oracle for one
+    candidate: the first beta-iteration t0 whose minimum cost (res_beta)
+    differs, and whether some iteration t <= t0 of the oracle had a near-tie
+    at the elite boundary (11th / 12th smallest QP cost) or at the argmin
+    (1st / 2nd) -- a flip there sends the two runs down different paths.
+    Returns (t0, near_tie, detail)."""
+    res = np.asarray(tr["res"], np.float64)
+    res_gpu = np.asarray(res_gpu, np.float64)
+    diff = ~(np.abs(res - res_gpu) <= 1e-6 * np.abs(res) + 1e-6)
+    # equal traces: an elite flip that left every minimum unchanged, or an
+    # argmin flip on the last iteration (other beta / sigma, same cost)
+    t0 = int(np.argmax(diff)) if diff.any() else len(res) - 1
+    for t in range(t0 + 1):
+        c = np.sort(np.asarray(tr["trace"][t]["cost"], np.float64))
+        for i in (0, 10):
+            gap = abs(c[i + 1] - c[i])
+            if gap <= tol * max(abs(c[i]), 1e-6):
+                return t0, True, f"beta-iteration {t}: sorted costs {i}/{i + 1} {c[i]:.9g} / {c[i + 1]:.9g}"
+    what = f"first res_beta difference at beta-iteration {t0}" if diff.any() else "res_beta traces agree"
+    return t0, False, f"{what}, no near-tie up to it"

@@ -9,13 +9,13 @@ import numpy as np
 import pytest
 
 import oracle
-from parity import DEFAULT_COV, DEFAULT_INIT, DEFAULT_MEAN, close, make_pair
+from parity import DEFAULT_COV, DEFAULT_INIT, DEFAULT_MEAN, beta_cem_trace, beta_near_tie, close, make_pair
 from test_gpu_parity_baseline import _sync_state
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("cost,noise,n,sample", [("mmd_opt", "gaussian", 22, [0, 341, 682, 1023]),
+@pytest.mark.parametrize("cost,noise,n,sample", [("mmd_opt", "gaussian", 22, list(range(0, 1024, 64))),
                                                  ("cvar", "beta", 500, list(range(0, 1024, 64)))])
 def test_full_shape_iteration(native, cost, noise, n, sample):
     B, O, H = 1024, 10, 30
@@ -40,11 +40,24 @@ def test_full_shape_iteration(native, cost, noise, n, sample):
     lane_g = nat.read("lane_cost")[:B]
     idx = np.array(sample)
     obs, lane, extra = ora.candidate_costs(cost, st, acc_g[idx], steer_g[idx], xo, yo, draws, 0)
-    # mmd_opt: 2000 QP-cost comparisons per candidate may flip a beta-CEM elite (costs agree ~1e-6), so one of
-    # the sampled candidates may differ; beta noise: rejection-sampler ulps, <= 5 % of candidates
-    frac = 0.25 if cost == "mmd_opt" else 0.05
-    close("obs_cost", obs_g[idx], obs, rtol=1e-3, atol=1e-2 if cost == "mmd_opt" else 1e-4, frac_ok=frac)
-    close("lane_cost", lane_g[idx], lane, rtol=1e-3, atol=1e-2 if cost == "mmd_opt" else 1e-4, frac_ok=frac)
+    if cost == "mmd_opt":
+        # 1e-4 relative per candidate; a candidate may differ only when its
+        # beta-CEM took another path at a reported near-tie of QP costs (the
+        # 2000 cost comparisons per candidate agree to ~1e-7 relative)
+        res_g = nat.read("res_beta").reshape(B, 20)
+        ok = np.abs(obs_g[idx] - obs) <= 1e-2 + 1e-4 * np.abs(obs)
+        ok &= np.abs(lane_g[idx] - lane) <= 1e-2 + 1e-4 * np.abs(lane)
+        for j in np.nonzero(~ok)[0]:
+            b = int(idx[j])
+            tr = beta_cem_trace(ora, st, acc_g[b], steer_g[b], draws, 0)
+            t0, tie, detail = beta_near_tie(tr, res_g[b])
+            print(f"candidate {b}: obs GPU {obs_g[b]} oracle {obs[j]}; {detail}")
+            assert tie, f"candidate {b}: obs {obs_g[b]} vs {obs[j]} not explained by a near-tie ({detail})"
+        assert ok.mean() >= 0.75, f"only {ok.sum()}/{ok.size} candidates agree"
+    else:
+        # beta noise: rejection-sampler ulps, <= 5 % of candidates
+        close("obs_cost", obs_g[idx], obs, rtol=1e-4, atol=1e-4, frac_ok=0.05)
+        close("lane_cost", lane_g[idx], lane, rtol=1e-4, atol=1e-4, frac_ok=0.05)
     # selection on the GPU's front / risk outputs: elite index sets exact
     pr_g = dict(res_norm=nat.read("res_norm")[:B], c_x=nat.read("cx").reshape(B, 11),
                 c_y=nat.read("cy").reshape(B, 11))

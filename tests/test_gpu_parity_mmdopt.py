@@ -84,11 +84,15 @@ def test_mother_features(native, noise):
     close("feat_cy", feat[:, 11:].transpose(0, 2, 1), cym, rtol=1e-4, atol=2e-4)
 
 
-@pytest.mark.parametrize("n,B,H,O,variant,check", [
-    (5, 20, 10, 3, "static", None), (12, 20, 10, 3, "static", [0, 7, 19]), (22, 20, 10, 3, "static", [0, 19]),
+@pytest.mark.parametrize("n,B,H,O,variant,check,qp_iters", [
+    (5, 20, 10, 3, "static", None, None), (12, 20, 10, 3, "static", [0, 7, 19], None),
+    (22, 20, 10, 3, "static", [0, 19], None),
     # BASELINE configs[3] shape: dynamic obstacles, H = 50, O = 20, n = 32 (M = 1024 mother rollouts)
-    (32, 20, 50, 20, "dynamic", [0, 19])])
-def test_beta_cem_lockstep(native, n, B, H, O, variant, check):
+    (32, 20, 50, 20, "dynamic", [0, 19], None),
+    # BASELINE configs[0] shape: n = 50 (M = 2500), B = 100, H = 20, O = 4 (the wave-per-QP path, n > 32);
+    # the oracle QP (100 x 50 x 2500 kernel entries per sample set) is checked on three iterations
+    (50, 100, 20, 4, "static", [0, 99], (0, 1, 19))])
+def test_beta_cem_lockstep(native, n, B, H, O, variant, check, qp_iters):
     ora, nat, xo, yo, draws, st, acc, steer = _run_mother(native, n, B, H, O, "gaussian", 2, variant)
     p = ora.prob
     M = n * n
@@ -96,6 +100,7 @@ def test_beta_cem_lockstep(native, n, B, H, O, variant, check):
     cand = list(range(B)) if check is None else check
     feat = nat.read("feat").reshape(B, 22, M)
     Fb = {b: np.ascontiguousarray(feat[b].T) for b in cand}        # [M, 22]
+    Db = {b: bc.distance_matrix(Fb[b]) for b in cand} if M > 256 else {b: None for b in cand}
     z0, z = draws.beta_z0, draws.beta_z
     samples = {}
     for b in cand:
@@ -113,8 +118,8 @@ def test_beta_cem_lockstep(native, n, B, H, O, variant, check):
         nat.run_stage(6, tb)
         btop = nat.read("btop").reshape(B, 100, n)
         bcost = nat.read("bcost").reshape(B, 100)
-        for b in cand:
-            beta, cost, _, _ = bc.reduced_qp(p, Fb[b], bsel[b].astype(np.int64), bsig[b], M)
+        for b in cand if qp_iters is None or tb in qp_iters else []:
+            beta, cost, _, _ = bc.reduced_qp(p, Fb[b], bsel[b].astype(np.int64), bsig[b], M, Db[b])
             close(f"btop[{tb},{b}]", btop[b], beta, rtol=1e-3, atol=1e-4)
             close(f"bcost[{tb},{b}]", bcost[b], cost, rtol=1e-4, atol=1e-4)
         nat.run_stage(7, tb)
@@ -151,24 +156,67 @@ def test_beta_cem_lockstep(native, n, B, H, O, variant, check):
     close("mmd_lane", nat.read("lane_cost")[:B], lane, rtol=1e-4, atol=1e-2)
 
 
-def test_mmdopt_iteration(native):
-    """Full GPU iterations (noise, front, mother, 20 x beta-CEM, final MMD,
-    select) against the oracle iteration on the GPU's carry.  The beta-CEM
-    makes 2000 QP-cost comparisons per candidate; costs agree to ~1e-6
-    relative, so an elite flip inside it (and a different beta / sigma) is
-    possible but rare: obs costs must agree for >= 90% of candidates."""
+def test_mmdopt_iteration_lockstep(native):
+    """20 full GPU mmd_opt iterations (noise, front, mother, 20 x beta-CEM,
+    final MMD, select).  Before each, the oracle is synchronised to the GPU's
+    carry and runs the same iteration.  Per candidate: obs / lane costs
+    within 1e-4 relative and the beta-CEM outputs (beta, sigma, res_beta)
+    equal; a candidate may differ only where its beta-CEM took another path
+    at a reported near-tie of QP costs.  Elite index sets (projection
+    permutation, obstacle elites, cost elites) exact unless a near-tie."""
+    from parity import beta_cem_trace, beta_near_tie
     from test_gpu_parity_baseline import _sync_state
-    n, B, H, O, Tf = 5, 24, 10, 3, 2
+    n, B, H, O, Tf = 6, 32, 10, 3, 20
     ora, nat, xo, yo = make_pair(native, "mmd_opt", "gaussian", n=n, O=O, H=H, B=B, T=Tf)
     draws = oracle.Draws.random(ora.prob, np.random.default_rng(4), idx_mpc=3, with_beta_cem=True)
     nat.begin("mmd_opt", 3, DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, xo, yo, 15.0, draws)
     st = ora.init_state(DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, draws)
+    exact, explained = 0, []
     for t in range(Tf):
         _sync_state(nat, st, B)
         st["pop"] = nat.read("pop")[(t & 1) * B * 8:(t & 1) * B * 8 + B * 8].reshape(B, 8).copy()
-        ora.iteration("mmd_opt", st, t, xo, yo, np.float32(15.0), draws, trace := [])
+        out = ora.iteration("mmd_opt", st, t, xo, yo, np.float32(15.0), draws, trace := [])
         tr = trace[0]
         nat.iterate(t, 1)
         nat.sync()
-        close(f"obs[{t}]", nat.read("obs_cost")[:B], tr["obs"], rtol=1e-3, atol=1e-2, frac_ok=0.1)
         close(f"res_norm[{t}]", nat.read("res_norm")[:B], tr["res_norm"], atol=1e-5)
+        obs_g, lane_g = nat.read("obs_cost")[:B], nat.read("lane_cost")[:B]
+        res_g = nat.read("res_beta").reshape(B, 20)
+        beta_g, sig_g = nat.read("beta").reshape(B, n), nat.read("sigma")[:B]
+        cost_ok = np.abs(obs_g - tr["obs"]) <= 1e-2 + 1e-4 * np.abs(tr["obs"])
+        cost_ok &= np.abs(lane_g - tr["lane"]) <= 1e-2 + 1e-4 * np.abs(tr["lane"])
+        ok = cost_ok & np.all(np.abs(res_g - tr["res_beta"]) <= 1e-4 * np.abs(tr["res_beta"]) + 1e-4, axis=1)
+        ok &= np.all(np.abs(beta_g - tr["beta"]) <= 1e-3 * np.abs(tr["beta"]) + 1e-4, axis=1)
+        ok &= np.abs(sig_g - tr["sigma"]) <= 1e-6 * np.abs(tr["sigma"])
+        if not ok.all():
+            acc, steer = nat.read("acc").reshape(B, 100), nat.read("steer").reshape(B, 100)
+            for b in np.nonzero(~ok)[0]:
+                t0, tie, detail = beta_near_tie(beta_cem_trace(ora, st, acc[b], steer[b], draws, t), res_g[b])
+                print(f"iteration {t} candidate {b}: obs {obs_g[b]} / {tr['obs'][b]}, sigma {sig_g[b]} / "
+                      f"{tr['sigma'][b]}; {detail}")
+                assert tie, f"iteration {t} candidate {b}: beta-CEM differs without a near-tie ({detail})"
+                explained.append((t, int(b)))
+        if not cost_ok.all():
+            continue  # obstacle / lane costs moved: the elite sets may legitimately differ; the next iteration re-syncs
+        tp = nat.read("tr_proj", np.int32).reshape(Tf, B)[t]
+        to = nat.read("tr_obs", np.int32).reshape(Tf, 20)[t]
+        tc = nat.read("tr_cem", np.int32).reshape(Tf, 5)[t]
+        if not elite_equal(f"elite_proj[{t}]", tp, tr["perm"], tr["res_norm"], tol=1e-3):
+            continue
+        if not elite_equal(f"elite_obs[{t}]", to, tr["elite_obs"], tr["obs"]):
+            continue
+        if not elite_equal(f"elite_cem[{t}]", tc, tr["elite_cem"], tr["cost20"]):
+            continue
+        exact += 1
+        nxt = ((t + 1) & 1) * B * 8
+        close(f"pop[{t}]", nat.read("pop")[nxt:nxt + B * 8].reshape(B, 8), st["pop"], rtol=1e-4, atol=1e-4)
+        res = nat.read("results").reshape(Tf, -1)[t]
+        close(f"result_cx[{t}]", res[:11], out["cx"], atol=1e-3)
+        close(f"result_cy[{t}]", res[11:22], out["cy"], atol=1e-3)
+        close(f"result_obs[{t}]", res[23], out["obs"], rtol=1e-4, atol=1e-2)
+        if ok[to[0]]:  # the result's beta-CEM outputs (unless that candidate's beta-CEM parted at a near-tie)
+            close(f"result_sigma[{t}]", res[24], out["sigma"], rtol=1e-6, atol=0)
+            close(f"result_res_beta[{t}]", res[25:45], out["res_beta"], rtol=1e-4, atol=1e-4)
+            close(f"result_beta[{t}]", res[45:45 + n], out["beta"], rtol=1e-3, atol=1e-4)
+    print(f"{exact}/{Tf} iterations exact; beta-CEM near-tie divergences {explained}")
+    assert exact >= 15, f"only {exact}/{Tf} iterations had identical elite sets"
