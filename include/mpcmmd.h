@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define MPCMMD_ABI_VERSION 1
+#define MPCMMD_ABI_VERSION 2
 
 /* status codes */
 #define MPCMMD_OK 0
@@ -117,6 +117,15 @@ int32_t mpcmmd_device_count(void);
 int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out);
 void mpcmmd_destroy(mpcmmd_handle* h);
 
+/* A handle that solves up to max_configs configurations of the same
+ * CEM(...) shape in one go (mpcmmd_solve_batch): every stage is ONE launch
+ * over (configuration x candidate), so the reference's num_batch = 100 sweep
+ * (S/main_mpc.py:106-128, 200 independent configurations) fills the GPU.
+ * Buffers are sized for max_configs * num_batch candidates (<= 65535).
+ * mpcmmd_create(cfg, out) == mpcmmd_create_batch(cfg, 1, out). */
+int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_handle** out);
+int32_t mpcmmd_max_configs(mpcmmd_handle* h);
+
 /* Run on a caller-owned hipStream_t instead of the handle's own stream. */
 int mpcmmd_set_stream(mpcmmd_handle* h, void* hip_stream);
 void* mpcmmd_get_stream(mpcmmd_handle* h);
@@ -141,6 +150,22 @@ int mpcmmd_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const flo
 int mpcmmd_iterate(mpcmmd_handle* h, int32_t t_begin, int32_t count);
 int mpcmmd_finish(mpcmmd_handle* h, mpcmmd_result* out);
 int mpcmmd_sync(mpcmmd_handle* h);
+
+/* n_cfg <= max_configs independent solves of the loop of S/main_mpc.py:106-128
+ * (compute_cem_* per configuration) in one batch.  Arrays carry a leading
+ * configuration axis: idx_mpc [n], init_state [n][6], mean [n][8], cov
+ * [n][64], x_obs / y_obs [n][O][100], v_des [n]; out [n].  Configuration g
+ * uses the internal RNG streams keyed by idx_mpc[g], so its result is
+ * bit-identical to mpcmmd_solve of that configuration alone (external draws
+ * are a single-configuration feature).  Synchronous. */
+int mpcmmd_solve_batch(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t* idx_mpc,
+                       const float* init_state, const float* mean, const float* cov, const float* x_obs,
+                       const float* y_obs, const float* v_des, mpcmmd_result* out);
+/* The batch split like begin / iterate / finish (iterate is shared). */
+int mpcmmd_begin_batch(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t* idx_mpc,
+                       const float* init_state, const float* mean, const float* cov, const float* x_obs,
+                       const float* y_obs, const float* v_des);
+int mpcmmd_finish_batch(mpcmmd_handle* h, int32_t n_cfg, mpcmmd_result* out);
 
 /* Per-kernel HIP-event timing (on the handle's stream).  When enabled, every
  * launch of every kernel is bracketed by events; mpcmmd_kernel_times returns,

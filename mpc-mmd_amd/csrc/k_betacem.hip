@@ -114,13 +114,14 @@ DEVI double row16_sum(double v) {
 __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = p.n, H = p.H, M = p.M, b = blockIdx.x;
+  const Cfg cf = cfg_of(p, b / p.B);
   float* an = reinterpret_cast<float*>(smem);
   float* sn = an + n * H;
   float* gctrl = p.ctrl_n + size_t(b) * 2 * n * H;
   for (int idx = threadIdx.x; idx < n * H; idx += blockDim.x) {
     const int r = idx / H, h = idx % H;
     float a, s;
-    noisy_control(p, t, r, h, p.acc[size_t(b) * 100 + h], p.steer[size_t(b) * 100 + h], a, s);
+    noisy_control(p, cf, t, r, h, p.acc[size_t(b) * 100 + h], p.steer[size_t(b) * 100 + h], a, s);
     an[idx] = a;
     sn[idx] = s;
     gctrl[idx] = a;
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
     // jnp.repeat(acc, n, 0) / jnp.tile(steer, (n, 1)) (cem_helper.py:510-511)
     const float* ar = an + (m / n) * H;
     const float* sr = sn + (m % n) * H;
-    float x = p.st0[0], y = p.st0[1], vx = p.st0[2], vy = p.st0[3], psi = p.st0[4];
+    float x = cf.st0[0], y = cf.st0[1], vx = cf.st0[2], vy = cf.st0[3], psi = cf.st0[4];
     double cx[11], cy[11];
 #pragma unroll
     for (int k = 0; k < 11; ++k) cx[k] = cy[k] = 0.0;
@@ -180,7 +181,7 @@ __global__ __launch_bounds__(kDistThreads) void k_bdist(Params p) {
   const int M = p.M, Md = dist_stride(M), T = (M + kDistRows - 1) / kDistRows;
   const int L = blockIdx.x, q = L / kXcds;
   const int b = (q / T) * kXcds + L % kXcds, r0 = (q % T) * kDistRows;
-  if (b >= p.B) return;
+  if (b >= p.Bt) return;
   const int tid = threadIdx.x;
   const float* Fg = p.feat + size_t(b) * kF * M;
   for (int i = tid; i < kDistRows * kF; i += kDistThreads) {
@@ -491,7 +492,7 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
   const int b = p.b0 + blockIdx.x, g = blockIdx.y, M = p.M, M1 = M + 1, n = p.n;
   int32_t* sel = p.bsel + size_t(b) * kBetaSamples * n;
   float* sig = p.bsig + size_t(b) * kBetaSamples;
-  const float* E = p.belite + (size_t(tb & 1) * p.B + b) * kBetaElite * M1;
+  const float* E = p.belite + (size_t(tb & 1) * p.Bt + b) * kBetaElite * M1;
   const int ys = ygen_stride(M);
   const float* Y = p.ygen + size_t(b) * kBzCols * ys;
   const float* z0 = p.beta_z0;
@@ -1048,8 +1049,8 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
   // ---- per position j: E_new column (the 11 elite sample values: previous
   // elites, this iteration's new samples (ygen) or, at tb = 0, the initial
   // samples), mean, u = (E - mean) / sqrt(10), block sums of u u^T
-  const float* Eold = p.belite + (size_t(tb & 1) * p.B + b) * kBetaElite * M1;
-  float* Enew = p.belite + (size_t((tb + 1) & 1) * p.B + b) * kBetaElite * M1;
+  const float* Eold = p.belite + (size_t(tb & 1) * p.Bt + b) * kBetaElite * M1;
+  float* Enew = p.belite + (size_t((tb + 1) & 1) * p.Bt + b) * kBetaElite * M1;
   const int ys = ygen_stride(M);
   const float* Y = p.ygen + size_t(b) * kBzCols * ys;
   const double rs10 = 1.0 / sqrt(10.0);
@@ -1268,17 +1269,18 @@ __global__ __launch_bounds__(64) void k_mmdfinal(Params p, int t) {
   __shared__ float cb[kMaxReduced], lb[kMaxReduced], ub[kMaxReduced], bt[kMaxReduced];
   __shared__ ReduceScratch rs;
   const int b = blockIdx.x, n = p.n, H = p.H, O = p.O, lane = threadIdx.x;
+  const Cfg cf = cfg_of(p, b / p.B);
   const float* ctrl = p.ctrl_n + size_t(b) * 2 * n * H;
   if (lane < n) {
     const int m = p.bestsel[size_t(b) * n + lane];
     const float* ar = ctrl + (m / n) * H;
     const float* sr = ctrl + n * H + (m % n) * H;
-    float x = p.st0[0], y = p.st0[1], vx = p.st0[2], vy = p.st0[3], psi = p.st0[4];
+    float x = cf.st0[0], y = cf.st0[1], vx = cf.st0[2], vy = cf.st0[3], psi = cf.st0[4];
     float c = 0.0f, l = 0.0f, u = 0.0f;
     bool nan = false;
     for (int h = 0; h < H; ++h) {
       for (int o = 0; o < O; ++o) {
-        const float f = f_bar(x, y, p.obs[o * H + h], p.obs[O * H + o * H + h]);
+        const float f = f_bar(x, y, cf.obs[o * H + h], cf.obs[O * H + o * H + h]);
         nan |= (f != f);
         c = fmaxf(c, f);
       }
@@ -1331,11 +1333,11 @@ bool mmdopt_supported(int n, int H, int O, std::string* why) {
 }
 
 void launch_mother(const Params& p, int t, hipStream_t s) {
-  hipLaunchKernelGGL(k_mother, dim3(p.B), dim3(kThreads), size_t(2) * p.n * p.H * 4, s, p, t);
+  hipLaunchKernelGGL(k_mother, dim3(p.Bt), dim3(kThreads), size_t(2) * p.n * p.H * 4, s, p, t);
 }
 
 void launch_bdist(const Params& p, hipStream_t s) {
-  const int T = (p.M + kDistRows - 1) / kDistRows, groups = (p.B + kXcds - 1) / kXcds;
+  const int T = (p.M + kDistRows - 1) / kDistRows, groups = (p.Bt + kXcds - 1) / kXcds;
   hipLaunchKernelGGL(k_bdist, dim3(groups * T * kXcds), dim3(kDistThreads), 0, s, p);
 }
 
@@ -1422,7 +1424,7 @@ void launch_belite(const Params& p, int tb, hipStream_t s) {
 }
 
 void launch_mmdfinal(const Params& p, int t, hipStream_t s) {
-  hipLaunchKernelGGL(k_mmdfinal, dim3(p.B), dim3(64), 0, s, p, t);
+  hipLaunchKernelGGL(k_mmdfinal, dim3(p.Bt), dim3(64), 0, s, p, t);
 }
 
 }  // namespace mpcmmd

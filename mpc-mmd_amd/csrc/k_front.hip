@@ -113,7 +113,8 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= p.B) return;
+  if (b >= p.Bt) return;
+  const double* solve_c = p.solve_c + size_t(b / p.B) * 4 * kNv;  // this candidate's configuration
   const int t0 = lane, t1 = lane + 64;
   const bool v1 = t1 < kN;
   const int t1c = v1 ? t1 : kN - 1;
@@ -129,7 +130,7 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
   }
 
   // ---- compute_x_guess: c_bar = G v + h (fp64) -------------------------------
-  const float* pop = p.pop + (size_t(t & 1) * p.B + b) * 8;
+  const float* pop = p.pop + (size_t(t & 1) * p.Bt + b) * 8;
   double cxb[kNv], cyb[kNv];
   float fcxb[kNv], fcyb[kNv];
   {
@@ -138,7 +139,7 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
     for (int j = 0; j < 8; ++j) v[j] = double(pop[j]);
 #pragma unroll
     for (int k = 0; k < kNv; ++k) {
-      double sx = p.solve_c[0 * kNv + k], sy = p.solve_c[1 * kNv + k];
+      double sx = solve_c[0 * kNv + k], sy = solve_c[1 * kNv + k];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         sx += p.guess_g[(0 * kNv + k) * 4 + j] * v[j];
@@ -236,7 +237,7 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
     // KKT solve: c = Kinv[:11,:11] (-lincost) + Kinv[:11,11:] b_eq
 #pragma unroll
     for (int k = 0; k < kNv; ++k) {
-      double sx = p.solve_c[2 * kNv + k], sy = p.solve_c[3 * kNv + k];
+      double sx = solve_c[2 * kNv + k], sy = solve_c[3 * kNv + k];
 #pragma unroll
       for (int j = 0; j < kNv; ++j) {
         sx += p.proj_m[(0 * kNv + k) * kNv + j] * (-double(linx[j]));
@@ -340,7 +341,7 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
 
   // ---- stores -----------------------------------------------------------------
   float* tr = p.traj;
-  const size_t plane = size_t(p.B) * kN;
+  const size_t plane = size_t(p.Bt) * kN;
   const size_t row = size_t(b) * kN;
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -377,7 +378,7 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
 }  // namespace
 
 void launch_front(const Params& p, int t, hipStream_t s) {
-  hipLaunchKernelGGL(k_front, dim3((p.B + 3) / 4), dim3(256), 0, s, p, t);
+  hipLaunchKernelGGL(k_front, dim3((p.Bt + 3) / 4), dim3(256), 0, s, p, t);
 }
 
 }  // namespace mpcmmd

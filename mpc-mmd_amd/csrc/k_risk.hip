@@ -78,9 +78,10 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
   const int O = p.O, H = p.H, S = p.S;
   RiskLds L = carve(smem, O, H, S);
   const int b = blockIdx.x;
+  const Cfg cf = cfg_of(p, b / p.B);
   for (int i = threadIdx.x; i < O * H; i += blockDim.x) {
-    L.xo[i] = p.obs[i];
-    L.yo[i] = p.obs[O * H + i];
+    L.xo[i] = cf.obs[i];
+    L.yo[i] = cf.obs[O * H + i];
   }
   for (int h = threadIdx.x; h < H; h += blockDim.x) {
     L.a[h] = p.acc[size_t(b) * 100 + h];
@@ -89,7 +90,7 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
   __syncthreads();
   const float* bpl = p.noise == 1 ? p.bplane + size_t(b) * 2 * H * S : nullptr;
   for (int r = threadIdx.x; r < S; r += blockDim.x) {
-    float x = p.st0[0], y = p.st0[1], vx = p.st0[2], vy = p.st0[3], psi = p.st0[4];
+    float x = cf.st0[0], y = cf.st0[1], vx = cf.st0[2], vy = cf.st0[3], psi = cf.st0[4];
     float cb = 0.0f, lb = 0.0f, ub = 0.0f;
     bool nan = false;
     for (int h = 0; h < H; ++h) {
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
       ub = fmaxf(ub, u1);
       if (h == H - 1) break;  // the last step's state is never recorded
       float an, sn;
-      noisy_control<true>(p, t, r, h, L.a[h], L.st[h], an, sn, bpl);
+      noisy_control<true>(p, cf, t, r, h, L.a[h], L.st[h], an, sn, bpl);
       bicycle_step(x, y, vx, vy, psi, an, sn);
     }
     const float qnan = __int_as_float(0x7fc00000);
@@ -142,14 +143,15 @@ __global__ __launch_bounds__(256) void k_gamma_tab(Params p, int t) {
   const int S = p.S, H = p.H;
   const int plane = S * H;
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx == 0) *p.bfix_n = 0u;  // k_beta_planes' deferred list of this iteration
+  const Cfg cf = cfg_of(p, blockIdx.y);
+  if (idx == 0 && blockIdx.y == 0) *p.bfix_n = 0u;  // k_beta_planes' deferred list of this iteration
   if (idx >= kGammaTabStreams * kGammaTabAttempts * plane) return;
   const int e = idx % plane, sk = idx / plane;
   const int k = sk % kGammaTabAttempts, st = sk / kGammaTabAttempts;
   const int h = e / S, r = e - h * S;
-  const uint32_t k0 = iteration_key0(p.idx_mpc, t), k1 = p.seed;
+  const uint32_t k0 = iteration_key0(cf.idx_mpc, t), k1 = p.seed;
   const GammaAttempt g = gamma_attempt(k0, k1, kStreamGammaAccA + uint32_t(st), uint32_t(r) * uint32_t(H) + h, k);
-  double* o = p.gtab + (size_t(sk) * 4) * plane + e;
+  double* o = cf.gtab + (size_t(sk) * 4) * plane + e;
   o[0] = g.x;
   o[plane] = g.u;
   o[2 * size_t(plane)] = g.lu;
@@ -163,6 +165,7 @@ __global__ __launch_bounds__(256) void k_gamma_tab(Params p, int t) {
 __global__ __launch_bounds__(256) void k_beta_planes(Params p, int t) {
   const int S = p.S, H = p.H;
   const int r = blockIdx.x * blockDim.x + threadIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const double* gtab = p.gtab + size_t(b / p.B) * gtab_stride(S, H);  // this candidate's configuration
   __shared__ MtConst mc[4];
   const float a = p.acc[size_t(b) * 100 + h], st = p.steer[size_t(b) * 100 + h];
   if (threadIdx.x < 4) {  // alphas 2|a|, 5|a|, 2|s|, 5|s| of this (candidate, step)
@@ -176,10 +179,10 @@ __global__ __launch_bounds__(256) void k_beta_planes(Params p, int t) {
   const size_t sl = size_t(kGammaTabAttempts) * 4 * S * H;
   const float fa = fabsf(a), fs = fabsf(st);
   float nba, nbs;
-  const bool ok = beta_draw_fast(double(2.0f * fa), double(5.0f * fa), 2.0, 5.0, mc[0], mc[1], p.gtab, p.gtab + sl,
+  const bool ok = beta_draw_fast(double(2.0f * fa), double(5.0f * fa), 2.0, 5.0, mc[0], mc[1], gtab, gtab + sl,
                                  S, H, r, h, nba) &&
-                  beta_draw_fast(double(2.0f * fs), double(5.0f * fs), 2.0, 5.0, mc[2], mc[3], p.gtab + 2 * sl,
-                                 p.gtab + 3 * sl, S, H, r, h, nbs);
+                  beta_draw_fast(double(2.0f * fs), double(5.0f * fs), 2.0, 5.0, mc[2], mc[3], gtab + 2 * sl,
+                                 gtab + 3 * sl, S, H, r, h, nbs);
   if (!ok) {
     const unsigned slot = atomicAdd(p.bfix_n, 1u);
     p.bfix[slot] = (uint32_t(b) * uint32_t(H) + uint32_t(h)) * uint32_t(S) + uint32_t(r);
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(256) void k_beta_fix(Params p, int t) {
     const int r = int(e % uint32_t(S)), bh = int(e / uint32_t(S));
     const int h = bh % H, b = bh / H;
     float nba, nbs;
-    beta_pair(p, t, r, h, p.acc[size_t(b) * 100 + h], p.steer[size_t(b) * 100 + h], nba, nbs);
+    beta_pair(p, cfg_of(p, b / p.B), t, r, h, p.acc[size_t(b) * 100 + h], p.steer[size_t(b) * 100 + h], nba, nbs);
     float* o = p.bplane + size_t(b) * 2 * H * S;
     o[size_t(h) * S + r] = nba;
     o[(size_t(H) + h) * S + r] = nbs;
@@ -209,19 +212,19 @@ __global__ __launch_bounds__(256) void k_beta_fix(Params p, int t) {
 }  // namespace
 
 void launch_beta_planes(const Params& p, int t, hipStream_t s) {
-  hipLaunchKernelGGL(k_beta_planes, dim3((p.S + 255) / 256, p.H, p.B), dim3(256), 0, s, p, t);
+  hipLaunchKernelGGL(k_beta_planes, dim3((p.S + 255) / 256, p.H, p.Bt), dim3(256), 0, s, p, t);
   hipLaunchKernelGGL(k_beta_fix, dim3(256), dim3(256), 0, s, p, t);
 }
 
 void launch_gamma_tab(const Params& p, int t, hipStream_t s) {
   const int total = kGammaTabStreams * kGammaTabAttempts * p.S * p.H;
-  hipLaunchKernelGGL(k_gamma_tab, dim3((total + 255) / 256), dim3(256), 0, s, p, t);
+  hipLaunchKernelGGL(k_gamma_tab, dim3((total + 255) / 256, p.G), dim3(256), 0, s, p, t);
 }
 
 void launch_risk_baseline(const Params& p, int t, hipStream_t s) {
   const size_t lds = risk_lds_bytes(p.O, p.H, p.S);
   const int threads = p.S >= 512 ? 512 : ((p.S + 63) / 64) * 64;
-  hipLaunchKernelGGL(k_risk_baseline, dim3(p.B), dim3(threads), lds, s, p, t);
+  hipLaunchKernelGGL(k_risk_baseline, dim3(p.Bt), dim3(threads), lds, s, p, t);
 }
 
 }  // namespace mpcmmd

@@ -31,35 +31,37 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
   __shared__ float mean32[8];
   __shared__ int imin_s;
   const int B = p.B;
+  const Cfg cf = cfg_of(p, blockIdx.x);  // one workgroup per configuration
+  const int g0 = blockIdx.x * B;          // its first candidate
   int N = 1;
   while (N < B) N <<= 1;
   const int tid = threadIdx.x;
 
   // ---- argsort(res_norm), stable ------------------------------------------
   for (int i = tid; i < N; i += blockDim.x)
-    keys[i] = i < B ? ((unsigned long long)sort_key(p.res_norm[i]) << 32) | unsigned(i) : ~0ull;
+    keys[i] = i < B ? ((unsigned long long)sort_key(p.res_norm[g0 + i]) << 32) | unsigned(i) : ~0ull;
   bitonic_sort(keys, N);
   for (int i = tid; i < B; i += blockDim.x) {
     perm[i] = int(keys[i] & 0xFFFFFFFFu);
-    p.tr_proj[size_t(t) * B + i] = perm[i];
+    cf.tr_proj[size_t(t) * B + i] = perm[i];
   }
   __syncthreads();
   // ---- argsort(obs cost) over the permuted batch -------------------------
   for (int i = tid; i < N; i += blockDim.x)
-    keys[i] = i < B ? ((unsigned long long)sort_key(p.obs_cost[perm[i]]) << 32) | unsigned(i) : ~0ull;
+    keys[i] = i < B ? ((unsigned long long)sort_key(p.obs_cost[g0 + perm[i]]) << 32) | unsigned(i) : ~0ull;
   bitonic_sort(keys, N);
   if (tid < kEliteCost) {
     const int e = perm[int(keys[tid] & 0xFFFFFFFFu)];
-    el[tid] = e;
-    p.tr_obs[size_t(t) * kEliteCost + tid] = e;
+    el[tid] = e;  // candidate index within the configuration
+    cf.tr_obs[size_t(t) * kEliteCost + tid] = e;
   }
   __syncthreads();
 
   // ---- compute_cost of the 20 elites: one wave each ----------------------
   const int lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
   for (int j = w; j < kEliteCost; j += nw) {
-    const int e = el[j];
-    const size_t plane = size_t(B) * kN, row = size_t(e) * kN;
+    const int e = g0 + el[j];
+    const size_t plane = size_t(p.Bt) * kN, row = size_t(e) * kN;
     const int t0 = lane, t1 = lane + 64;
     const bool v1 = t1 < kN;
     const int t1c = v1 ? t1 : kN - 1;
@@ -87,7 +89,7 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
       n_des += dd * dd;
       n_st += double(st[q]) * double(st[q]);
       const float v = sqrtf(xd[q] * xd[q] + yd[q] * yd[q]);
-      const double dv = double(v - p.v_des);
+      const double dv = double(v - cf.v_des);
       n_v += dv * dv;
       const double sp = double(fmaxf(0.0f, fabsf(st[q]) - 0.6f));
       n_sp += sp * sp;
@@ -129,8 +131,8 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
     if (r < kElite) cem5[r] = tid;
   }
   __syncthreads();
-  const float* pop = p.pop + size_t(t & 1) * B * 8;
-  float* pop_next = p.pop + size_t((t + 1) & 1) * B * 8;
+  const float* pop = p.pop + (size_t(t & 1) * p.Bt + g0) * 8;
+  float* pop_next = p.pop + (size_t((t + 1) & 1) * p.Bt + g0) * 8;
   if (tid < kElite * 8) {
     const int q = tid >> 3, c = tid & 7;
     pe[q][c] = pop[size_t(el[cem5[q]]) * 8 + c];
@@ -151,7 +153,7 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
     for (int c = 0; c < 8; ++c) {
       double s = 0.0;
       for (int q = 0; q < kElite; ++q) s += wgt[q] * double(pe[q][c]);
-      m32[c] = float((1.0 - 0.6) * double(p.mean[c]) + 0.6 * s / sw);
+      m32[c] = float((1.0 - 0.6) * double(cf.mean[c]) + 0.6 * s / sw);
       mean32[c] = m32[c];
     }
     double cv[8][8];
@@ -160,11 +162,11 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
         double s = 0.0;
         for (int q = 0; q < kElite; ++q)
           s += wgt[q] * (double(pe[q][a]) - double(m32[a])) * (double(pe[q][c]) - double(m32[c]));
-        const float v = float((1.0 - 0.6) * double(p.cov[a * 8 + c]) + 0.6 * s / sw + (a == c ? 0.01 : 0.0));
+        const float v = float((1.0 - 0.6) * double(cf.cov[a * 8 + c]) + 0.6 * s / sw + (a == c ? 0.01 : 0.0));
         cv[a][c] = double(v);
-        p.cov[a * 8 + c] = v;
+        cf.cov[a * 8 + c] = v;
       }
-    for (int c = 0; c < 8; ++c) p.mean[c] = m32[c];
+    for (int c = 0; c < 8; ++c) cf.mean[c] = m32[c];
     // Cholesky (lower) of the fp32 covariance, in fp64
     for (int j = 0; j < 8; ++j) {
       double d = cv[j][j];
@@ -186,11 +188,11 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
         break;
       }
     imin_s = im;
-    for (int q = 0; q < kElite; ++q) p.tr_cem[size_t(t) * kElite + q] = cem5[q];
+    for (int q = 0; q < kElite; ++q) cf.tr_cem[size_t(t) * kElite + q] = cem5[q];
   }
   __syncthreads();
   // ---- new population: [elites; mean + L z], v columns clipped -----------
-  const float* z = p.resample + size_t(t) * (B - kElite) * 8;
+  const float* z = cf.resample + size_t(t) * (B - kElite) * 8;
   for (int i = tid; i < B; i += blockDim.x) {
     float row[8];
     if (i < kElite) {
@@ -208,8 +210,8 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
   }
   // ---- per-iteration result (cem.py:314-315) ------------------------------
   if (tid < kResultStride) {
-    const int e = el[imin_s];
-    float* r = p.results + size_t(t) * kResultStride;
+    const int e = g0 + el[imin_s];
+    float* r = cf.results + size_t(t) * kResultStride;
     float v = 0.0f;
     if (tid < 11) v = p.cx[size_t(e) * 11 + tid];
     else if (tid < 22) v = p.cy[size_t(e) * 11 + tid - 11];
@@ -225,12 +227,13 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
 // internal draws of outer iteration t: roll [3][H][S] and resample [B-5][8]
 __global__ __launch_bounds__(256) void k_noise(Params p, int t) {
   const int S = p.S, H = p.H;
-  const uint32_t k0 = iteration_key0(p.idx_mpc, t), k1 = p.seed;
+  const Cfg cf = cfg_of(p, blockIdx.y);  // configuration blockIdx.y, keyed by its own idx_mpc
+  const uint32_t k0 = iteration_key0(cf.idx_mpc, t), k1 = p.seed;
   const int nroll = (S * H + 3) / 4;
   const int nres = ((p.B - kElite) * 8 + 3) / 4;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  float* roll = const_cast<float*>(p.roll) + size_t(t) * 3 * H * S;
-  float* res = const_cast<float*>(p.resample) + size_t(t) * (p.B - kElite) * 8;
+  float* roll = const_cast<float*>(cf.roll) + size_t(t) * 3 * H * S;
+  float* res = const_cast<float*>(cf.resample) + size_t(t) * (p.B - kElite) * 8;
   if (j < 3 * nroll) {
     const int st = j / nroll, jb = j % nroll;
     double z[4];
@@ -255,14 +258,14 @@ __global__ __launch_bounds__(256) void k_noise(Params p, int t) {
 }  // namespace
 
 void launch_select(const Params& p, int t, hipStream_t s) {
-  hipLaunchKernelGGL(k_select, dim3(1), dim3(1024), 0, s, p, t);
+  hipLaunchKernelGGL(k_select, dim3(p.G), dim3(1024), 0, s, p, t);
 }
 
 void launch_noise(const Params& p, int t, hipStream_t s) {
   const int nroll = (p.S * p.H + 3) / 4;
   const int nres = ((p.B - kElite) * 8 + 3) / 4;
   const int total = 3 * nroll + nres;
-  hipLaunchKernelGGL(k_noise, dim3((total + 255) / 256), dim3(256), 0, s, p, t);
+  hipLaunchKernelGGL(k_noise, dim3((total + 255) / 256, p.G), dim3(256), 0, s, p, t);
 }
 
 }  // namespace mpcmmd

@@ -35,42 +35,48 @@ HDI_CONST int pos_pad(int M) { return ((M + 1) + 31) & ~31; }  // whole pairs of
 HDI_CONST int dist_stride(int M) { return (M + 31) & ~31; }
 
 struct Params {
-  // shapes / configuration
+  // shapes / configuration.  A launch covers G configurations of B
+  // candidates each (mpcmmd_solve_batch; G = 1 for mpcmmd_solve): candidate
+  // arrays are indexed by the global candidate b in [0, Bt), Bt = G B, and
+  // the per-configuration arrays below are [G][...] (cfg_of)
   int32_t B, S, H, O, n, M, T;
+  int32_t G, Bt;
   int32_t cost;      // MPCMMD_COST_*
   int32_t noise;     // MPCMMD_NOISE_*
-  int32_t idx_mpc;
   uint32_t seed;
   // candidate range of one beta-CEM launch: [b0, b0 + nb) (the beta-iteration
   // kernels run per candidate group, each group on its own stream)
   int32_t b0, nb;
   float sigma_acc, sigma_steer, acc_const, steer_const, K_steer;
-  float y_lb, y_ub, v_des;
+  float y_lb, y_ub;
   float w_obs, w_lane;
   // constants (device)
   const float* basis;      // [3][100][11] fp32: P, Pd, Pdd
   const double* guess_g;   // [2][11][4]  (x: v-columns, y: y-columns)
   const double* proj_m;    // [2][11][11] (Kinv[:11,:11] for x, y)
   const double* fit;       // [11][H]
-  const double* solve_c;   // [4][11] per solve: guess h_x, h_y, proj e_x, e_y
-  const float* obs;        // [2][O][H] x_obs, y_obs (first H columns)
-  const float* st0;        // [5] initial rollout state
+  // per configuration
+  const int32_t* idx_mpc;  // [G]
+  const float* v_des;      // [G]
+  const double* solve_c;   // [G][4][11] per solve: guess h_x, h_y, proj e_x, e_y
+  const float* obs;        // [G][2][O][H] x_obs, y_obs (first H columns)
+  const float* st0;        // [G][8] initial rollout state
   // noise tables, device layout (iteration-major, sample-minor for coalescing)
-  const float* roll;       // [T][3][H][S]
-  const float* resample;   // [T][B-5][8]
-  float* bplane;           // [B][2][H][S] Beta draws (acc, steer) of the baseline rollouts (beta noise)
-  uint32_t* bfix;          // [B*H*S] elements k_beta_planes deferred to k_beta_fix
+  const float* roll;       // [G][T][3][H][S]
+  const float* resample;   // [G][T][B-5][8]
+  float* bplane;           // [Bt][2][H][S] Beta draws (acc, steer) of the baseline rollouts (beta noise)
+  uint32_t* bfix;          // [Bt*H*S] elements k_beta_planes deferred to k_beta_fix
   uint32_t* bfix_n;        // their count (zeroed by k_gamma_tab)
-  double* gtab;            // Beta-noise attempt table of the current iteration (rng.hpp: gamma_tab_size)
+  double* gtab;            // [G][gamma_tab_size] Beta-noise attempt tables of the current iteration
   const float* beta_z0;    // [100][M+1]
   const double* beta_z;    // [20][pos_pad(M)][kBzCols] fp32 normals held as fp64 (position-major, zero padded)
   // carry / state
-  float* pop;              // [2][B][8] double-buffered population
-  float* mean;             // [8]
-  float* cov;              // [64]
-  float* lam_x;            // [B][11]
-  float* lam_y;            // [B][11]
-  float* s_lane;           // [B][198]
+  float* pop;              // [2][Bt][8] double-buffered population
+  float* mean;             // [G][8]
+  float* cov;              // [G][64]
+  float* lam_x;            // [Bt][11]
+  float* lam_y;            // [Bt][11]
+  float* s_lane;           // [Bt][198]
   // per-iteration intermediates
   float* cx;               // [B][11]
   float* cy;               // [B][11]
@@ -107,11 +113,51 @@ struct Params {
   // [0] distinct distance rows staged, [1] (sample, reduced row) pairs summed
   unsigned long long* stats;  // [8]
   // outputs
-  float* results;          // [T][kResultStride]
-  int32_t* tr_proj;        // [T][B]
-  int32_t* tr_obs;         // [T][20]
-  int32_t* tr_cem;         // [T][5]
+  float* results;          // [G][T][kResultStride]
+  int32_t* tr_proj;        // [G][T][B]
+  int32_t* tr_obs;         // [G][T][20]
+  int32_t* tr_cem;         // [G][T][5]
 };
+
+// The slices of configuration g (candidates [g B, (g + 1) B)).
+struct Cfg {
+  int g;
+  int32_t idx_mpc;
+  float v_des;
+  const double* solve_c;
+  const float* obs;
+  const float* st0;
+  const float* roll;
+  const float* resample;
+  double* gtab;
+  float* mean;
+  float* cov;
+  float* results;
+  int32_t* tr_proj;
+  int32_t* tr_obs;
+  int32_t* tr_cem;
+};
+HDI_CONST size_t gtab_stride(int S, int H) { return size_t(4) * 4 * 4 * S * H; }  // == gamma_tab_size (rng.hpp)
+__device__ inline Cfg cfg_of(const Params& p, int g) {
+  Cfg c;
+  const size_t T = size_t(p.T), H = size_t(p.H), S = size_t(p.S), O = size_t(p.O);
+  c.g = g;
+  c.idx_mpc = p.idx_mpc[g];
+  c.v_des = p.v_des[g];
+  c.solve_c = p.solve_c + size_t(g) * 4 * 11;
+  c.obs = p.obs + size_t(g) * 2 * O * H;
+  c.st0 = p.st0 + size_t(g) * 8;
+  c.roll = p.roll + size_t(g) * T * 3 * H * S;
+  c.resample = p.resample + size_t(g) * T * (p.B - 5) * 8;
+  c.gtab = p.gtab ? p.gtab + size_t(g) * gtab_stride(p.S, p.H) : nullptr;
+  c.mean = p.mean + size_t(g) * 8;
+  c.cov = p.cov + size_t(g) * 64;
+  c.results = p.results + size_t(g) * T * kResultStride;
+  c.tr_proj = p.tr_proj + size_t(g) * T * p.B;
+  c.tr_obs = p.tr_obs + size_t(g) * T * kEliteCost;
+  c.tr_cem = p.tr_cem + size_t(g) * T * kElite;
+  return c;
+}
 
 void launch_noise(const Params& p, int t, hipStream_t s);
 void launch_front(const Params& p, int t, hipStream_t s);

@@ -73,6 +73,8 @@ struct mpcmmd_handle {
   bool own_stream = false;
   Params p{};
   int B = 0, S = 0, H = 0, O = 0, n = 0, M = 0, T = 0;
+  int Gmax = 1;  // configurations the buffers hold (mpcmmd_create_batch)
+  int G = 1;     // configurations of the current solve
   std::map<std::string, std::pair<void*, size_t>> bufs;
   // solve state
   int cost = -1;
@@ -188,21 +190,21 @@ void upload(mpcmmd_handle* h, const char* name, const void* src, size_t bytes, s
 
 // upload through the handle's pinned staging area (mpcmmd_begin): src may be
 // a host temporary, the copy still runs after the call returns
-void upload_staged(mpcmmd_handle* h, const char* name, const void* src, size_t bytes) {
+void upload_staged(mpcmmd_handle* h, const char* name, const void* src, size_t bytes, size_t offset = 0) {
   const size_t at = (h->stage_used + 63) & ~size_t(63);
   if (at + bytes > h->stage_bytes) throw std::runtime_error(std::string("staging area too small for ") + name);
   std::memcpy(h->stage + at, src, bytes);
   h->stage_used = at + bytes;
-  upload(h, name, h->stage + at, bytes);
+  upload(h, name, h->stage + at, bytes, offset);
 }
 
 // bytes of staging mpcmmd_begin needs at most (each piece 64-byte aligned)
-size_t stage_size(int B, int S, int H, int O, int T) {
+size_t stage_size(int B, int S, int H, int O, int T, int G) {
   const size_t pieces[] = {size_t(4) * 11 * 8, 8 * 4, size_t(2) * O * H * 4, size_t(B) * 8 * 4, 8 * 4, 64 * 4,
-                           size_t(T) * 3 * H * S * 4, size_t(T) * (B - kElite) * 8 * 4};
+                           size_t(T) * 3 * H * S * 4, size_t(T) * (B - kElite) * 8 * 4, 4, 4};
   size_t s = 0;
-  for (size_t b : pieces) s += (b + 63) & ~size_t(63);
-  return s + 64;
+  for (size_t b : pieces) s += size_t(G) * b;
+  return s + 16 * 64;
 }
 
 // beta_z iteration t: [89][M+1] (draw order) -> device [pos_pad(M)][kBzCols]
@@ -244,7 +246,7 @@ void run_beta_iteration(mpcmmd_handle* h, const Params& p, int tb, hipStream_t s
 // stream (profiling runs them on the handle's stream, one after another,
 // so the HIP-event timings are per kernel)
 void run_beta_cem(mpcmmd_handle* h) {
-  const int B = h->B, G = h->prof ? 1 : h->groups;
+  const int B = h->p.Bt, G = h->prof ? 1 : h->groups;  // every candidate of every configuration
   if (G <= 1) {
     for (int tb = 0; tb < kBetaIters; ++tb) run_beta_iteration(h, h->p, tb, h->stream);
     return;
@@ -345,7 +347,9 @@ int32_t mpcmmd_device_count(void) {
   return n;
 }
 
-int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
+int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) { return mpcmmd_create_batch(cfg, 1, out); }
+
+int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_handle** out) {
   if (!cfg || !out) return fail(MPCMMD_E_INVALID, "null argument");
   *out = nullptr;
   const mpcmmd_config& c = *cfg;
@@ -356,6 +360,11 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
                 "config out of range (num_reduced>=2, num_obs>=1, 2<=num_prime<=100, 20<=num_batch<=4096)");
   if (c.num_reduced > 1024) return fail(MPCMMD_E_UNSUPPORTED, "num_reduced > 1024");
   if (size_t(c.num_obs) * c.num_prime > 8192) return fail(MPCMMD_E_UNSUPPORTED, "num_obs * num_prime > 8192");
+  if (max_configs < 1) return fail(MPCMMD_E_INVALID, "max_configs must be >= 1");
+  // grid limits: candidates on grid y / z (<= 65535), Beta fix-up list entries (32-bit)
+  const size_t Bt = size_t(max_configs) * c.num_batch;
+  if (Bt > 65535 || Bt * c.num_prime * c.num_reduced >= (size_t(1) << 32))
+    return fail(MPCMMD_E_UNSUPPORTED, "max_configs * num_batch too large (<= 65535 candidates per handle)");
   auto* h = new mpcmmd_handle();
   int rc = guarded([&] {
     h->cfg = c;
@@ -374,7 +383,12 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
     h->n = c.num_reduced;
     h->M = c.num_reduced * c.num_reduced;
     h->T = c.maxiter_cem;
+    h->Gmax = max_configs;
+    h->G = 1;
     const int B = h->B, S = h->S, H = h->H, O = h->O, T = h->T;
+    const int GM = h->Gmax;
+    const size_t BT = size_t(GM) * B;  // candidate capacity
+    if (gtab_stride(S, H) != gamma_tab_size(S, H)) throw std::logic_error("Beta attempt table stride");
     const bool mmd_ok = mmdopt_supported(h->n, h->H, h->O, &h->mmd_why);
     h->mmd_ok = mmd_ok;
     Params& p = h->p;
@@ -387,6 +401,8 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
     p.T = T;
     p.noise = c.noise;
     p.seed = c.seed;
+    p.G = 1;
+    p.Bt = B;
     p.b0 = 0;
     p.nb = B;
     p.sigma_acc = c.noise_level;
@@ -429,60 +445,62 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
     }
     p.proj_m = (const double*)h->alloc("proj_m", pm.size() * 8);
     p.fit = (const double*)h->alloc("fit", h->pc.fit.size() * 8);
-    p.solve_c = (const double*)h->alloc("solve_c", 4 * kNvar * 8);
-    p.obs = (const float*)h->alloc("obs", size_t(2) * O * H * 4);
-    p.st0 = (const float*)h->alloc("st0", 8 * 4);
-    p.roll = (const float*)h->alloc("roll", size_t(T) * 3 * H * S * 4);
-    p.resample = (const float*)h->alloc("resample", size_t(T) * (B - kElite) * 8 * 4);
-    p.bplane = (float*)h->alloc("bplane", c.noise == MPCMMD_NOISE_BETA ? size_t(B) * 2 * H * S * 4 : 16);
-    p.bfix = (uint32_t*)h->alloc("bfix", c.noise == MPCMMD_NOISE_BETA ? size_t(B) * H * S * 4 : 16);
+    p.solve_c = (const double*)h->alloc("solve_c", size_t(GM) * 4 * kNvar * 8);
+    p.obs = (const float*)h->alloc("obs", size_t(GM) * 2 * O * H * 4);
+    p.st0 = (const float*)h->alloc("st0", size_t(GM) * 8 * 4);
+    p.idx_mpc = (const int32_t*)h->alloc("idx_mpc", size_t(GM) * 4);
+    p.v_des = (const float*)h->alloc("v_des", size_t(GM) * 4);
+    p.roll = (const float*)h->alloc("roll", size_t(GM) * T * 3 * H * S * 4);
+    p.resample = (const float*)h->alloc("resample", size_t(GM) * T * (B - kElite) * 8 * 4);
+    p.bplane = (float*)h->alloc("bplane", c.noise == MPCMMD_NOISE_BETA ? BT * 2 * H * S * 4 : 16);
+    p.bfix = (uint32_t*)h->alloc("bfix", c.noise == MPCMMD_NOISE_BETA ? BT * H * S * 4 : 16);
     p.bfix_n = (uint32_t*)h->alloc("bfix_n", 16);
-    p.gtab = (double*)h->alloc("gtab", c.noise == MPCMMD_NOISE_BETA ? gamma_tab_size(S, H) * 8 : 16);
+    p.gtab = c.noise == MPCMMD_NOISE_BETA ? (double*)h->alloc("gtab", size_t(GM) * gamma_tab_size(S, H) * 8) : nullptr;
     if (mmd_ok) {
       p.beta_z0 = (const float*)h->alloc("beta_z0", size_t(kBetaSamples) * (h->M + 1) * 4);
       p.beta_z = (const double*)h->alloc("beta_z", size_t(kBetaIters) * pos_pad(h->M) * kBzCols * 8);
       const size_t M = h->M, M1 = M + 1, n = h->n;
-      p.feat = (float*)h->alloc("feat", size_t(B) * 22 * M * 4);
-      p.bdist = (float*)h->alloc("bdist", size_t(B) * M * dist_stride(int(M)) * 4);
-      p.ctrl_n = (float*)h->alloc("ctrl_n", size_t(B) * 2 * n * H * 4);
-      p.bsel = (int32_t*)h->alloc("bsel", size_t(B) * kBetaSamples * n * 4);
-      p.bsig = (float*)h->alloc("bsig", size_t(B) * kBetaSamples * 4);
-      p.btop = (float*)h->alloc("btop", size_t(B) * kBetaSamples * n * 4);
-      p.bcost = (float*)h->alloc("bcost", size_t(B) * kBetaSamples * 4);
-      p.belite = (float*)h->alloc("belite", size_t(2) * B * kBetaElite * M1 * 4);
+      p.feat = (float*)h->alloc("feat", BT * 22 * M * 4);
+      p.bdist = (float*)h->alloc("bdist", BT * M * dist_stride(int(M)) * 4);
+      p.ctrl_n = (float*)h->alloc("ctrl_n", BT * 2 * n * H * 4);
+      p.bsel = (int32_t*)h->alloc("bsel", BT * kBetaSamples * n * 4);
+      p.bsig = (float*)h->alloc("bsig", BT * kBetaSamples * 4);
+      p.btop = (float*)h->alloc("btop", BT * kBetaSamples * n * 4);
+      p.bcost = (float*)h->alloc("bcost", BT * kBetaSamples * 4);
+      p.belite = (float*)h->alloc("belite", size_t(2) * BT * kBetaElite * M1 * 4);
       const size_t Pp = pos_pad(h->M);
-      p.gen = (double*)h->alloc("gen", size_t(B) * Pp * kGenStride * 8);
-      p.genm = (double*)h->alloc("genm", size_t(B) * Pp * 8);
-      p.phib = (double*)h->alloc("phib", size_t(B) * ((h->M + 1 + 15) / 16) * 66 * 8);
-      p.bimin = (int32_t*)h->alloc("bimin", size_t(B) * 4);
-      p.bestsel = (int32_t*)h->alloc("bestsel", size_t(B) * n * 4);
-      p.brow = (double*)h->alloc("brow", size_t(B) * kBetaSamples * n * 8);
-      p.bkred = (float*)h->alloc("bkred", size_t(B) * kBetaSamples * (n * (n - 1) / 2) * 4);
-      p.ygen = (float*)h->alloc("ygen", size_t(B) * kBzCols * ygen_stride(h->M) * 4);
+      p.gen = (double*)h->alloc("gen", BT * Pp * kGenStride * 8);
+      p.genm = (double*)h->alloc("genm", BT * Pp * 8);
+      p.phib = (double*)h->alloc("phib", BT * ((h->M + 1 + 15) / 16) * 66 * 8);
+      p.bimin = (int32_t*)h->alloc("bimin", BT * 4);
+      p.bestsel = (int32_t*)h->alloc("bestsel", BT * n * 4);
+      p.brow = (double*)h->alloc("brow", BT * kBetaSamples * n * 8);
+      p.bkred = (float*)h->alloc("bkred", BT * kBetaSamples * (n * (n - 1) / 2) * 4);
+      p.ygen = (float*)h->alloc("ygen", BT * kBzCols * ygen_stride(h->M) * 4);
     }
-    p.pop = (float*)h->alloc("pop", size_t(2) * B * 8 * 4);
-    p.mean = (float*)h->alloc("mean", 8 * 4);
-    p.cov = (float*)h->alloc("cov", 64 * 4);
-    p.lam_x = (float*)h->alloc("lam_x", size_t(B) * kNvar * 4);
-    p.lam_y = (float*)h->alloc("lam_y", size_t(B) * kNvar * 4);
-    p.s_lane = (float*)h->alloc("s_lane", size_t(B) * kLane * 4);
-    p.cx = (float*)h->alloc("cx", size_t(B) * kNvar * 4);
-    p.cy = (float*)h->alloc("cy", size_t(B) * kNvar * 4);
-    p.traj = (float*)h->alloc("traj", size_t(6) * B * kNum * 4);
-    p.res_norm = (float*)h->alloc("res_norm", size_t(B) * 4);
-    p.acc = (float*)h->alloc("acc", size_t(B) * kNum * 4);
-    p.steer = (float*)h->alloc("steer", size_t(B) * kNum * 4);
-    p.obs_cost = (float*)h->alloc("obs_cost", size_t(B) * 4);
-    p.lane_cost = (float*)h->alloc("lane_cost", size_t(B) * 4);
-    p.beta = (float*)h->alloc("beta", size_t(B) * h->n * 4);
-    p.sigma = (float*)h->alloc("sigma", size_t(B) * 4);
-    p.res_beta = (float*)h->alloc("res_beta", size_t(B) * kBetaIters * 4);
+    p.pop = (float*)h->alloc("pop", size_t(2) * BT * 8 * 4);
+    p.mean = (float*)h->alloc("mean", size_t(GM) * 8 * 4);
+    p.cov = (float*)h->alloc("cov", size_t(GM) * 64 * 4);
+    p.lam_x = (float*)h->alloc("lam_x", BT * kNvar * 4);
+    p.lam_y = (float*)h->alloc("lam_y", BT * kNvar * 4);
+    p.s_lane = (float*)h->alloc("s_lane", BT * kLane * 4);
+    p.cx = (float*)h->alloc("cx", BT * kNvar * 4);
+    p.cy = (float*)h->alloc("cy", BT * kNvar * 4);
+    p.traj = (float*)h->alloc("traj", size_t(6) * BT * kNum * 4);
+    p.res_norm = (float*)h->alloc("res_norm", BT * 4);
+    p.acc = (float*)h->alloc("acc", BT * kNum * 4);
+    p.steer = (float*)h->alloc("steer", BT * kNum * 4);
+    p.obs_cost = (float*)h->alloc("obs_cost", BT * 4);
+    p.lane_cost = (float*)h->alloc("lane_cost", BT * 4);
+    p.beta = (float*)h->alloc("beta", BT * h->n * 4);
+    p.sigma = (float*)h->alloc("sigma", BT * 4);
+    p.res_beta = (float*)h->alloc("res_beta", BT * kBetaIters * 4);
     p.dbg = (unsigned long long*)h->alloc("dbg", 64 * 8);
     p.stats = (unsigned long long*)h->alloc("stats", 8 * 8);
-    p.results = (float*)h->alloc("results", size_t(T) * kResultStride * 4);
-    p.tr_proj = (int32_t*)h->alloc("tr_proj", size_t(T) * B * 4);
-    p.tr_obs = (int32_t*)h->alloc("tr_obs", size_t(T) * kEliteCost * 4);
-    p.tr_cem = (int32_t*)h->alloc("tr_cem", size_t(T) * kElite * 4);
+    p.results = (float*)h->alloc("results", size_t(GM) * T * kResultStride * 4);
+    p.tr_proj = (int32_t*)h->alloc("tr_proj", size_t(GM) * T * B * 4);
+    p.tr_obs = (int32_t*)h->alloc("tr_obs", size_t(GM) * T * kEliteCost * 4);
+    p.tr_cem = (int32_t*)h->alloc("tr_cem", size_t(GM) * T * kElite * 4);
     if (const char* g = std::getenv("MPCMMD_GROUPS")) h->groups = std::max(1, std::min(mpcmmd_handle::kMaxGroups, std::atoi(g)));
     if (h->groups > 1) {
       HIPC(hipEventCreateWithFlags(&h->gev_start, hipEventDisableTiming));
@@ -491,7 +509,7 @@ int mpcmmd_create(const mpcmmd_config* cfg, mpcmmd_handle** out) {
         HIPC(hipEventCreateWithFlags(&h->gev_done[g], hipEventDisableTiming));
       }
     }
-    h->stage_bytes = stage_size(B, S, H, O, T);
+    h->stage_bytes = stage_size(B, S, H, O, T, GM);
     HIPC(hipHostMalloc(reinterpret_cast<void**>(&h->stage), h->stage_bytes, hipHostMallocDefault));
     HIPC(hipEventCreateWithFlags(&h->stage_ev, hipEventDisableTiming));
     upload(h, "basis", basis.data(), basis.size() * 4);
@@ -545,16 +563,23 @@ int mpcmmd_set_stream(mpcmmd_handle* h, void* s) {
 
 void* mpcmmd_get_stream(mpcmmd_handle* h) { return h ? (void*)h->stream : nullptr; }
 
-int mpcmmd_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const float init_state[6],
-                 const float mean[8], const float cov[64], const float* x_obs, const float* y_obs, float v_des,
-                 const mpcmmd_draws* draws) {
-  if (!h || !init_state || !mean || !cov || !x_obs || !y_obs) return fail(MPCMMD_E_INVALID, "null argument");
+namespace {
+
+// mpcmmd_begin for n configurations (arrays with a leading configuration
+// axis); external draws only for n == 1 (the parity contract)
+int begin_impl(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t* idx_mpc, const float* init_state,
+               const float* mean, const float* cov, const float* x_obs, const float* y_obs, const float* v_des,
+               const mpcmmd_draws* draws) {
+  if (!h || !idx_mpc || !init_state || !mean || !cov || !x_obs || !y_obs || !v_des)
+    return fail(MPCMMD_E_INVALID, "null argument");
   if (cost_kind < 0 || cost_kind > 3) return fail(MPCMMD_E_INVALID, "cost_kind must be 0..3");
+  if (n_cfg < 1 || n_cfg > h->Gmax) return fail(MPCMMD_E_INVALID, "n_cfg must be 1..max_configs of the handle");
+  if (draws && n_cfg > 1) return fail(MPCMMD_E_INVALID, "external draws need n_cfg == 1");
   if (cost_kind == MPCMMD_COST_MMD_OPT && !h->mmd_ok) return fail(MPCMMD_E_UNSUPPORTED, h->mmd_why);
   return guarded([&] {
     check_device(h);
     Params& p = h->p;
-    const int B = h->B, S = h->S, H = h->H, O = h->O, T = h->T;
+    const int B = h->B, S = h->S, H = h->H, O = h->O, T = h->T, G = n_cfg;
     if (h->stage_pending) HIPC(hipEventSynchronize(h->stage_ev));  // previous begin's copies done
     h->stage_pending = false;
     h->stage_used = 0;
@@ -567,56 +592,69 @@ int mpcmmd_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const flo
       }
     } drain{h};
     h->cost = cost_kind;
+    h->G = G;
     p.cost = cost_kind;
-    p.idx_mpc = idx_mpc;
-    p.v_des = v_des;
+    p.G = G;
+    p.Bt = G * B;
+    p.b0 = 0;
+    p.nb = p.Bt;
     // cem.py:161-163 weights (obs, lane)
     const float w_obs[4] = {1e3f, 1e3f, 1e3f, 1e6f}, w_lane[4] = {0.f, 0.f, 0.f, 1e6f};
     p.w_obs = w_obs[cost_kind];
     p.w_lane = w_lane[cost_kind];
-    // boundary vectors (cem_helper.py:152-167) and the per-solve KKT columns
-    const double bx[3] = {init_state[0], init_state[2], init_state[4]};
-    const double by[4] = {init_state[1], init_state[3], init_state[5], 0.0};
-    std::vector<double> sc(4 * kNvar, 0.0);
-    for (int k = 0; k < kNvar; ++k) {
-      for (int e = 0; e < 3; ++e) sc[0 * kNvar + k] += h->pc.guess_kinv_x[k * 14 + kNvar + e] * bx[e];
-      for (int e = 0; e < 4; ++e) sc[1 * kNvar + k] += h->pc.guess_kinv_y[k * 15 + kNvar + e] * by[e];
-      for (int e = 0; e < 3; ++e) sc[2 * kNvar + k] += h->pc.proj_kinv_x[k * 14 + kNvar + e] * bx[e];
-      for (int e = 0; e < 4; ++e) sc[3 * kNvar + k] += h->pc.proj_kinv_y[k * 15 + kNvar + e] * by[e];
-    }
-    upload_staged(h, "solve_c", sc.data(), sc.size() * 8);
-    float st0[8] = {init_state[0], init_state[1], init_state[2], init_state[3],
-                    atan2f(init_state[3], init_state[2]), 0.f, 0.f, 0.f};
-    upload_staged(h, "st0", st0, sizeof(st0));
-    std::vector<float> ob(size_t(2) * O * H);
-    for (int o = 0; o < O; ++o)
-      for (int t = 0; t < H; ++t) {
-        ob[size_t(o) * H + t] = x_obs[o * kNum + t];
-        ob[size_t(O) * H + o * H + t] = y_obs[o * kNum + t];
-      }
-    upload_staged(h, "obs", ob.data(), ob.size() * 4);
-    // sampling_param (cem_helper.py:122-150): fixed key
+    upload_staged(h, "idx_mpc", idx_mpc, size_t(G) * 4);
+    upload_staged(h, "v_des", v_des, size_t(G) * 4);
+    // sampling_param (cem_helper.py:122-150): fixed key, the same draws for every configuration
     std::vector<float> z0;
     if (draws && draws->pop0) z0.assign(draws->pop0, draws->pop0 + size_t(B) * 8);
     else z0 = host_normals(kFixedKey0, h->cfg.seed, kStreamPop0, 0, size_t(B) * 8);
-    double cv[64], L[64];
-    for (int i = 0; i < 64; ++i) cv[i] = double(cov[i]);
-    if (!chol8(cv, L)) throw std::invalid_argument("cov_param_init is not positive definite");
-    std::vector<float> pop(size_t(B) * 8);
-    for (int b = 0; b < B; ++b)
-      for (int a = 0; a < 8; ++a) {
-        double s = double(mean[a]);
-        for (int c = 0; c <= a; ++c) s += L[a * 8 + c] * double(z0[size_t(b) * 8 + c]);
-        float v = float(s);
-        if (a < 4) v = fminf(fmaxf(v, 0.1f), 30.0f);
-        pop[size_t(b) * 8 + a] = v;
+    std::vector<double> sc(size_t(G) * 4 * kNvar, 0.0);
+    std::vector<float> st0(size_t(G) * 8, 0.f), ob(size_t(G) * 2 * O * H), pop(size_t(G) * B * 8);
+    for (int g = 0; g < G; ++g) {
+      const float* is = init_state + size_t(g) * 6;
+      // boundary vectors (cem_helper.py:152-167) and the per-solve KKT columns
+      const double bx[3] = {is[0], is[2], is[4]};
+      const double by[4] = {is[1], is[3], is[5], 0.0};
+      double* scg = sc.data() + size_t(g) * 4 * kNvar;
+      for (int k = 0; k < kNvar; ++k) {
+        for (int e = 0; e < 3; ++e) scg[0 * kNvar + k] += h->pc.guess_kinv_x[k * 14 + kNvar + e] * bx[e];
+        for (int e = 0; e < 4; ++e) scg[1 * kNvar + k] += h->pc.guess_kinv_y[k * 15 + kNvar + e] * by[e];
+        for (int e = 0; e < 3; ++e) scg[2 * kNvar + k] += h->pc.proj_kinv_x[k * 14 + kNvar + e] * bx[e];
+        for (int e = 0; e < 4; ++e) scg[3 * kNvar + k] += h->pc.proj_kinv_y[k * 15 + kNvar + e] * by[e];
       }
-    upload_staged(h, "pop", pop.data(), pop.size() * 4);
-    upload_staged(h, "mean", mean, 8 * 4);
-    upload_staged(h, "cov", cov, 64 * 4);
-    HIPC(hipMemsetAsync(p.lam_x, 0, size_t(B) * kNvar * 4, h->stream));
-    HIPC(hipMemsetAsync(p.lam_y, 0, size_t(B) * kNvar * 4, h->stream));
-    HIPC(hipMemsetAsync(p.s_lane, 0, size_t(B) * kLane * 4, h->stream));
+      float* s0 = st0.data() + size_t(g) * 8;
+      s0[0] = is[0], s0[1] = is[1], s0[2] = is[2], s0[3] = is[3], s0[4] = atan2f(is[3], is[2]);
+      const float* xo = x_obs + size_t(g) * O * kNum;
+      const float* yo = y_obs + size_t(g) * O * kNum;
+      float* obg = ob.data() + size_t(g) * 2 * O * H;
+      for (int o = 0; o < O; ++o)
+        for (int t = 0; t < H; ++t) {
+          obg[size_t(o) * H + t] = xo[o * kNum + t];
+          obg[size_t(O) * H + o * H + t] = yo[o * kNum + t];
+        }
+      const float* mg = mean + size_t(g) * 8;
+      double cv[64], L[64];
+      for (int i = 0; i < 64; ++i) cv[i] = double(cov[size_t(g) * 64 + i]);
+      if (!chol8(cv, L)) throw std::invalid_argument("cov_param_init is not positive definite");
+      float* pg = pop.data() + size_t(g) * B * 8;
+      for (int b = 0; b < B; ++b)
+        for (int a = 0; a < 8; ++a) {
+          double s = double(mg[a]);
+          for (int c = 0; c <= a; ++c) s += L[a * 8 + c] * double(z0[size_t(b) * 8 + c]);
+          float v = float(s);
+          if (a < 4) v = fminf(fmaxf(v, 0.1f), 30.0f);
+          pg[size_t(b) * 8 + a] = v;
+        }
+    }
+    upload_staged(h, "solve_c", sc.data(), sc.size() * 8);
+    upload_staged(h, "st0", st0.data(), st0.size() * 4);
+    upload_staged(h, "obs", ob.data(), ob.size() * 4);
+    upload_staged(h, "pop", pop.data(), pop.size() * 4);  // iteration 0's half: [0][G B][8]
+    upload_staged(h, "mean", mean, size_t(G) * 8 * 4);
+    upload_staged(h, "cov", cov, size_t(G) * 64 * 4);
+    HIPC(hipMemsetAsync(p.lam_x, 0, size_t(G) * B * kNvar * 4, h->stream));
+    HIPC(hipMemsetAsync(p.lam_y, 0, size_t(G) * B * kNvar * 4, h->stream));
+    HIPC(hipMemsetAsync(p.s_lane, 0, size_t(G) * B * kLane * 4, h->stream));
     // external noise rows: [T][3][S][H] -> device [T][3][H][S]
     h->ext_roll = draws && draws->roll;
     h->ext_res = draws && draws->resample;
@@ -652,6 +690,45 @@ int mpcmmd_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const flo
   });
 }
 
+// the result of configuration g (cem.py:324-333): the last enqueued iteration
+void read_result(mpcmmd_handle* h, int g, mpcmmd_result* out) {
+  const int T = h->T;
+  std::vector<float> r(kResultStride);
+  HIPC(hipMemcpy(r.data(), h->p.results + (size_t(g) * T + h->last_t) * kResultStride, kResultStride * 4,
+                 hipMemcpyDeviceToHost));
+  std::memcpy(out->cx, &r[0], 11 * 4);
+  std::memcpy(out->cy, &r[11], 11 * 4);
+  out->cost_lane = r[22];
+  out->cost_obs = r[23];
+  out->sigma = r[24];
+  std::memcpy(out->res_beta, &r[25], 20 * 4);
+  if (out->beta && h->cost == MPCMMD_COST_MMD_OPT) std::memcpy(out->beta, &r[45], size_t(h->n) * 4);
+  const int Tr = h->last_t + 1;
+  if (out->elite_proj)
+    HIPC(hipMemcpy(out->elite_proj, h->p.tr_proj + size_t(g) * T * h->B, size_t(Tr) * h->B * 4,
+                   hipMemcpyDeviceToHost));
+  if (out->elite_obs)
+    HIPC(hipMemcpy(out->elite_obs, h->p.tr_obs + size_t(g) * T * kEliteCost, size_t(Tr) * kEliteCost * 4,
+                   hipMemcpyDeviceToHost));
+  if (out->elite_cem)
+    HIPC(hipMemcpy(out->elite_cem, h->p.tr_cem + size_t(g) * T * kElite, size_t(Tr) * kElite * 4,
+                   hipMemcpyDeviceToHost));
+}
+
+}  // namespace
+
+int mpcmmd_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const float init_state[6],
+                 const float mean[8], const float cov[64], const float* x_obs, const float* y_obs, float v_des,
+                 const mpcmmd_draws* draws) {
+  return begin_impl(h, 1, cost_kind, &idx_mpc, init_state, mean, cov, x_obs, y_obs, &v_des, draws);
+}
+
+int mpcmmd_begin_batch(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t* idx_mpc,
+                       const float* init_state, const float* mean, const float* cov, const float* x_obs,
+                       const float* y_obs, const float* v_des) {
+  return begin_impl(h, n_cfg, cost_kind, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des, nullptr);
+}
+
 int mpcmmd_iterate(mpcmmd_handle* h, int32_t t_begin, int32_t count) {
   if (!h) return fail(MPCMMD_E_INVALID, "null handle");
   if (!h->begun) return fail(MPCMMD_E_STATE, "mpcmmd_iterate before mpcmmd_begin");
@@ -682,30 +759,17 @@ int mpcmmd_sync(mpcmmd_handle* h) {
   });
 }
 
-int mpcmmd_finish(mpcmmd_handle* h, mpcmmd_result* out) {
+int mpcmmd_finish(mpcmmd_handle* h, mpcmmd_result* out) { return mpcmmd_finish_batch(h, 1, out); }
+
+int mpcmmd_finish_batch(mpcmmd_handle* h, int32_t n_cfg, mpcmmd_result* out) {
   if (!h || !out) return fail(MPCMMD_E_INVALID, "null argument");
   if (!h->begun || h->last_t < 0) return fail(MPCMMD_E_STATE, "no iteration has run");
+  if (n_cfg < 1 || n_cfg > h->G) return fail(MPCMMD_E_INVALID, "n_cfg exceeds the configurations of the solve");
   return guarded([&] {
     check_device(h);
     HIPC(hipStreamSynchronize(h->stream));
     if (h->prof) h->collect();
-    std::vector<float> r(kResultStride);
-    HIPC(hipMemcpy(r.data(), h->p.results + size_t(h->last_t) * kResultStride, kResultStride * 4,
-                   hipMemcpyDeviceToHost));
-    std::memcpy(out->cx, &r[0], 11 * 4);
-    std::memcpy(out->cy, &r[11], 11 * 4);
-    out->cost_lane = r[22];
-    out->cost_obs = r[23];
-    out->sigma = r[24];
-    std::memcpy(out->res_beta, &r[25], 20 * 4);
-    if (out->beta && h->cost == MPCMMD_COST_MMD_OPT) std::memcpy(out->beta, &r[45], size_t(h->n) * 4);
-    const int T = h->last_t + 1;
-    if (out->elite_proj)
-      HIPC(hipMemcpy(out->elite_proj, h->p.tr_proj, size_t(T) * h->B * 4, hipMemcpyDeviceToHost));
-    if (out->elite_obs)
-      HIPC(hipMemcpy(out->elite_obs, h->p.tr_obs, size_t(T) * kEliteCost * 4, hipMemcpyDeviceToHost));
-    if (out->elite_cem)
-      HIPC(hipMemcpy(out->elite_cem, h->p.tr_cem, size_t(T) * kElite * 4, hipMemcpyDeviceToHost));
+    for (int g = 0; g < n_cfg; ++g) read_result(h, g, out + g);
     return MPCMMD_OK;
   });
 }
@@ -719,6 +783,18 @@ int mpcmmd_solve(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const flo
   if (rc) return rc;
   return mpcmmd_finish(h, out);
 }
+
+int mpcmmd_solve_batch(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t* idx_mpc,
+                       const float* init_state, const float* mean, const float* cov, const float* x_obs,
+                       const float* y_obs, const float* v_des, mpcmmd_result* out) {
+  int rc = mpcmmd_begin_batch(h, n_cfg, cost_kind, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des);
+  if (rc) return rc;
+  rc = mpcmmd_iterate(h, 0, h->T);
+  if (rc) return rc;
+  return mpcmmd_finish_batch(h, n_cfg, out);
+}
+
+int32_t mpcmmd_max_configs(mpcmmd_handle* h) { return h ? h->Gmax : 0; }
 
 int mpcmmd_profile(mpcmmd_handle* h, int32_t enable) {
   if (!h) return fail(MPCMMD_E_INVALID, "null handle");

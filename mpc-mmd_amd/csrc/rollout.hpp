@@ -13,10 +13,10 @@ constexpr float kWheelBase = 2.5f;   // cem.py:26
 // (cem_helper.py:427-433): Beta(2|a|, 5|a|), Beta(2|s|, 5|s|).  mc: the four
 // Marsaglia-Tsang constants of (2|a|, 5|a|, 2|s|, 5|s|) when the caller
 // shares them across rows (else computed here).
-DEVI void beta_pair(const Params& p, int t, int r, int h, float a, float s, float& nba, float& nbs,
+DEVI void beta_pair(const Params& p, const Cfg& cf, int t, int r, int h, float a, float s, float& nba, float& nbs,
                     const MtConst* mc = nullptr) {
   const int S = p.S, H = p.H;
-  const uint32_t k0 = iteration_key0(p.idx_mpc, t), k1 = p.seed;
+  const uint32_t k0 = iteration_key0(cf.idx_mpc, t), k1 = p.seed;
   const size_t sl = size_t(kGammaTabAttempts) * 4 * S * H;  // one stream's table
   const float fa = fabsf(a), fs = fabsf(s);
   const double aa = double(2.0f * fa), ab = double(5.0f * fa), sa = double(2.0f * fs), sb = double(5.0f * fs);
@@ -26,9 +26,9 @@ DEVI void beta_pair(const Params& p, int t, int r, int h, float a, float s, floa
   } else {
     m[0] = mt_const(aa), m[1] = mt_const(ab), m[2] = mt_const(sa), m[3] = mt_const(sb);
   }
-  nba = beta_draw_tab(aa, ab, 2.0, 5.0, m[0], m[1], p.gtab, p.gtab + sl, S, H, r, h, k0, k1, kStreamGammaAccA,
+  nba = beta_draw_tab(aa, ab, 2.0, 5.0, m[0], m[1], cf.gtab, cf.gtab + sl, S, H, r, h, k0, k1, kStreamGammaAccA,
                       kStreamGammaAccB);
-  nbs = beta_draw_tab(sa, sb, 2.0, 5.0, m[2], m[3], p.gtab + 2 * sl, p.gtab + 3 * sl, S, H, r, h, k0, k1,
+  nbs = beta_draw_tab(sa, sb, 2.0, 5.0, m[2], m[3], cf.gtab + 2 * sl, cf.gtab + 3 * sl, S, H, r, h, k0, k1,
                       kStreamGammaSteerA, kStreamGammaSteerB);
 }
 
@@ -39,10 +39,10 @@ DEVI void beta_pair(const Params& p, int t, int r, int h, float a, float s, floa
 // iteration's attempt table p.gtab (k_gamma_tab).
 // kPlanes: Beta draws read from bpl (k_beta_planes) instead of sampled here.
 template <bool kPlanes = false>
-DEVI void noisy_control(const Params& p, int t, int r, int h, float a, float s, float& an, float& sn,
+DEVI void noisy_control(const Params& p, const Cfg& cf, int t, int r, int h, float a, float s, float& an, float& sn,
                         const float* bpl = nullptr) {
   const int S = p.S, H = p.H;
-  const float* roll = p.roll + size_t(t) * 3 * H * S;
+  const float* roll = cf.roll + size_t(t) * 3 * H * S;
   const float nc = roll[(2 * H + h) * S + r];
   float ap, sp;
   if (p.noise == 0) {
@@ -54,7 +54,7 @@ DEVI void noisy_control(const Params& p, int t, int r, int h, float a, float s, 
       nba = bpl[size_t(h) * S + r];
       nbs = bpl[(size_t(H) + h) * S + r];
     } else {
-      beta_pair(p, t, r, h, a, s, nba, nbs);
+      beta_pair(p, cf, t, r, h, a, s, nba, nbs);
     }
     ap = p.sigma_acc * (2.0f * nba - 1.0f);
     sp = p.K_steer * (2.0f * nbs - 1.0f);  // K_steer holds float32(K_steer * sigma_steer)

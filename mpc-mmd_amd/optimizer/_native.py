@@ -18,14 +18,15 @@ COST = {"mmd_opt": 0, "mmd_random": 1, "cvar": 2, "saa": 3}
 NOISE = {"gaussian": 0, "beta": 1}
 VARIANT = {"static": 0, "dynamic": 1}
 RESULT_STRIDE_BETA_MAX = 32
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 SYMBOLS = (
     "mpcmmd_abi_version", "mpcmmd_last_error", "mpcmmd_device_count", "mpcmmd_create",
     "mpcmmd_destroy", "mpcmmd_set_stream", "mpcmmd_get_stream", "mpcmmd_solve", "mpcmmd_begin",
     "mpcmmd_iterate", "mpcmmd_finish", "mpcmmd_sync", "mpcmmd_profile", "mpcmmd_kernel_times",
     "mpcmmd_kernel_name", "mpcmmd_buffer_info", "mpcmmd_read", "mpcmmd_write", "mpcmmd_run_stage",
-    "mpcmmd_host_constant", "mpcmmd_obs_dynamic_traj", "mpcmmd_validate",
+    "mpcmmd_host_constant", "mpcmmd_obs_dynamic_traj", "mpcmmd_validate", "mpcmmd_create_batch",
+    "mpcmmd_max_configs", "mpcmmd_solve_batch", "mpcmmd_begin_batch", "mpcmmd_finish_batch",
 )
 
 
@@ -83,6 +84,14 @@ def lib():
     L.mpcmmd_last_error.restype = C.c_char_p
     L.mpcmmd_device_count.restype = C.c_int32
     L.mpcmmd_create.argtypes = [C.POINTER(Config), C.POINTER(vp)]
+    L.mpcmmd_create_batch.argtypes = [C.POINTER(Config), C.c_int32, C.POINTER(vp)]
+    L.mpcmmd_max_configs.argtypes = [vp]
+    L.mpcmmd_max_configs.restype = C.c_int32
+    ip = C.POINTER(C.c_int32)
+    bargs = [vp, C.c_int32, C.c_int32, ip, fp, fp, fp, fp, fp, fp]
+    L.mpcmmd_solve_batch.argtypes = bargs + [C.POINTER(Result)]
+    L.mpcmmd_begin_batch.argtypes = bargs
+    L.mpcmmd_finish_batch.argtypes = [vp, C.c_int32, C.POINTER(Result)]
     L.mpcmmd_destroy.argtypes = [vp]
     L.mpcmmd_destroy.restype = None
     L.mpcmmd_set_stream.argtypes = [vp, vp]
@@ -178,15 +187,17 @@ def _fptr(a):
 
 
 class Handle:
-    """Owns one mpcmmd_handle (one device, one stream)."""
+    """Owns one mpcmmd_handle (one device, one stream).  ``max_configs`` > 1
+    sizes it for ``solve_batch`` (that many configurations per launch)."""
 
-    def __init__(self, cfg):
+    def __init__(self, cfg, max_configs=1):
         self.cfg = cfg
+        self.max_configs = int(max_configs)
         self._L = lib()
         if self._L.mpcmmd_device_count() < 1:
             raise NativeError("no HIP device visible: libmpcmmd needs an MI355X (gfx950)")
         h = C.c_void_p()
-        check(self._L.mpcmmd_create(C.byref(cfg), C.byref(h)))
+        check(self._L.mpcmmd_create_batch(C.byref(cfg), self.max_configs, C.byref(h)))
         self._h = h
         self._keep = []
 
@@ -251,6 +262,50 @@ class Handle:
         if tr is not None:
             out.update(tr)
         return out
+
+    def _batch_inputs(self, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des):
+        G = len(idx_mpc)
+        if G > self.max_configs:
+            raise ValueError(f"{G} configurations > max_configs {self.max_configs}")
+        f = lambda a, *sh: np.ascontiguousarray(np.broadcast_to(np.asarray(a, np.float32), sh))
+        O = self.cfg.num_obs
+        ins = dict(idx=np.ascontiguousarray(np.asarray(idx_mpc, np.int64).astype(np.int32)),
+                   init=f(init_state, G, 6) if np.ndim(init_state) == 2 else f(np.asarray(init_state).reshape(6), G, 6),
+                   mean=f(mean, G, 8) if np.ndim(mean) == 2 else f(np.asarray(mean).reshape(8), G, 8),
+                   cov=f(np.asarray(cov, np.float32).reshape(-1, 64), G, 64),
+                   xo=f(np.asarray(x_obs, np.float32).reshape(G, O, 100), G, O, 100),
+                   yo=f(np.asarray(y_obs, np.float32).reshape(G, O, 100), G, O, 100),
+                   vd=f(np.asarray(v_des, np.float32).reshape(-1), G))
+        args = (ins["idx"].ctypes.data_as(C.POINTER(C.c_int32)), _fptr(ins["init"]), _fptr(ins["mean"]),
+                _fptr(ins["cov"]), _fptr(ins["xo"]), _fptr(ins["yo"]), _fptr(ins["vd"]))
+        return G, ins, args
+
+    def begin_batch(self, cost, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des):
+        """mpcmmd_begin_batch (then iterate / finish_batch)."""
+        G, ins, args = self._batch_inputs(idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des)
+        self._keep = [ins]
+        check(self._L.mpcmmd_begin_batch(self._h, G, COST[cost], *args))
+        self._G = G
+
+    def finish_batch(self):
+        G = self._G
+        rs = (Result * G)()
+        betas = [np.zeros(max(self.cfg.num_reduced, 1), np.float32) for _ in range(G)]
+        for g in range(G):
+            rs[g].beta = _fptr(betas[g])
+        check(self._L.mpcmmd_finish_batch(self._h, G, rs))
+        return [dict(cx=np.array(r.cx, np.float32), cy=np.array(r.cy, np.float32),
+                     cost_lane=np.float32(r.cost_lane), cost_obs=np.float32(r.cost_obs), sigma=np.float32(r.sigma),
+                     res_beta=np.array(r.res_beta, np.float32), beta=betas[g]) for g, r in enumerate(rs)]
+
+    def solve_batch(self, cost, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des):
+        """mpcmmd_solve_batch: len(idx_mpc) configurations in one batch.
+        init_state / mean / cov / v_des may be shared (one value) or per
+        configuration; x_obs, y_obs [G, O, 100].  Returns one result dict
+        per configuration (the keys of finish())."""
+        self.begin_batch(cost, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des)
+        self.iterate(0, self.cfg.maxiter_cem)
+        return self.finish_batch()
 
     def solve(self, cost, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des, draws=None, trace=False):
         self.begin(cost, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des, draws)

@@ -160,6 +160,25 @@ def run_block_concurrent(prob, handles, cost, ids, init_state, mean, cov, v_des=
     return np.stack(rows) if rows else np.zeros((0, row_width(prob.num_reduced)), np.float32)
 
 
+def run_block_batch(prob, handle, cost, ids, init_state, mean, cov, v_des=15.0, variant="static"):
+    """Solve configs ``ids`` with handle.max_configs configurations per
+    batch (mpcmmd_solve_batch: every kernel is one launch over
+    configuration x candidate).  Rows are identical to run_block's: every
+    configuration's RNG is keyed by its own idx_mpc."""
+    rows = []
+    G = handle.max_configs
+    ids = list(ids)
+    for g0 in range(0, len(ids), G):
+        group = ids[g0:g0 + G]
+        obs = [obstacles(variant, k, prob.num_obs) for k in group]
+        tr = [tracks(prob, ob) for ob in obs]
+        res = handle.solve_batch(cost, [ob["idx_mpc"] for ob in obs], init_state, mean, cov,
+                                 np.stack([t[0] for t in tr]), np.stack([t[1] for t in tr]), v_des)
+        for k, r in zip(group, res):
+            rows.append(pack(k, result_tuple(cost, r, prob.num_reduced), prob.num_reduced))
+    return np.stack(rows) if rows else np.zeros((0, row_width(prob.num_reduced)), np.float32)
+
+
 def save_npz(path, rows, cost, num_obs, init_state, variant="static"):
     """Successful configs in the reference's layout (S/main_mpc.py:130-135;
     dynamic: D/main_mpc.py:150-156 adds psi_obs, x_obs_traj, y_obs_traj)."""
@@ -192,7 +211,9 @@ def main():
     ap.add_argument("--acc-const-noise", type=float, default=0.0)
     ap.add_argument("--steer-const-noise", type=float, default=0.0)
     ap.add_argument("--out", default="")
-    ap.add_argument("--streams", type=int, default=8, help="configurations in flight per GPU (1 = one at a time)")
+    ap.add_argument("--batch", type=int, default=32,
+                    help="configurations per batched solve (mpcmmd_solve_batch; 0 = use --streams)")
+    ap.add_argument("--streams", type=int, default=1, help="with --batch 0: configurations in flight on streams")
     ap.add_argument("--variant", default="static", choices=["static", "dynamic"])
     a = ap.parse_args()
 
@@ -215,7 +236,13 @@ def main():
     mean = np.array([15.0] * 4 + [0.0] * 4, np.float32)                 # :56-71
     cov = np.diag([20.0] * 4 + [100.0] * 4).astype(np.float32)          # :69-74
     ids = shard(a.num_configs, world, rank)
-    if a.streams > 1:
+    if a.batch > 0:
+        from . import _native
+        G = max(1, min(a.batch, len(ids), 65535 // a.num_batch))
+        hb = _native.Handle(prob._cfg, max_configs=G)
+        rows = run_block_batch(prob, hb, a.cost, ids, init, mean, cov, variant=a.variant)
+        hb.close()
+    elif a.streams > 1:
         from . import _native
         hs = [prob.handle] + [_native.Handle(prob._cfg) for _ in range(a.streams - 1)]
         rows = run_block_concurrent(prob, hs, a.cost, ids, init, mean, cov, variant=a.variant)

@@ -26,3 +26,26 @@ def test_concurrent_equals_sequential(cost, n, variant):
     con = run_block_concurrent(prob, hs, cost, ids, init, mean, cov, variant=variant)
     assert np.array_equal(seq, con)
     assert np.all(np.isfinite(seq[:, 1:25]))
+
+
+@pytest.mark.parametrize("variant", ["static", "dynamic"])
+@pytest.mark.parametrize("cost,n,noise", [("cvar", 32, "gaussian"), ("mmd_opt", 8, "gaussian"), ("cvar", 24, "beta"),
+                                          ("mmd_random", 16, "gaussian")])
+def test_batch_equals_sequential(cost, n, noise, variant):
+    """mpcmmd_solve_batch (one launch per stage over configuration x
+    candidate): rows bit-identical to one-configuration solves, including a
+    last batch that is only partly filled (7 configurations, batches of 3)."""
+    from optimizer import _native
+    from optimizer.cem import CEM
+    from optimizer.sweep import run_block, run_block_batch
+    prob = CEM(n, 4, 0.1 if noise == "gaussian" else 0.3, 20, noise, 0.0, 0.0, num_batch=100, device=0,
+               variant=variant)
+    init = np.array([0.0, 1.75 if variant == "static" else -1.75, 5.0, 0.0, 0.0, 0.0], np.float32)
+    mean = np.array([15.0] * 4 + [0.0] * 4, np.float32)
+    cov = np.diag([20.0] * 4 + [100.0] * 4).astype(np.float32)
+    ids = range(7)
+    seq = run_block(prob, cost, ids, init, mean, cov, variant=variant)
+    hb = _native.Handle(prob._cfg, max_configs=3)
+    bat = run_block_batch(prob, hb, cost, ids, init, mean, cov, variant=variant)
+    hb.close()
+    assert np.array_equal(seq, bat), np.argwhere(seq != bat)[:5]
