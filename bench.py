@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Throughput bench of the CEM-projection optimizer hot path (BASELINE.json).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload mmd_opt|cvar]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload mmd_opt|cvar|dynamic|configs0]
 
 One step = one outer CEM iteration (cem.py:221-315 body: initial guess,
 projection, controls, noisy rollouts, risk reducer (beta-CEM for mmd_opt),
@@ -9,7 +9,8 @@ elite sorts, CEM update) over the whole batch, on device-resident inputs, with
 the library's internal Philox noise.  Every 20 steps a new solve starts
 (mpcmmd_begin: boundary vectors, initial population, obstacle upload), as in
 the reference's 20-iteration compute_cem_* call; that host work is inside the
-timed region.
+timed region.  ``value`` = K / elapsed of the K timed steps; the per-step
+HIP-event durations give ``median_ms_per_step``.
 
 N > 1: one process per GPU (torchrun).  Each rank solves its own obstacle
 configuration (config k = rank, seeded like S/main_mpc.py:12,114), so per-GPU
@@ -17,9 +18,12 @@ work is fixed ("scaling": "weak"); RCCL is used for the barrier, the max of
 the elapsed times and the final gather of the per-config results (§8e).
 
 Extra fields: "roofline" for the dominant kernel (HIP-event durations of the
-library's launches on its stream, during a profiled pass of the same steps)
-and "cpu_baseline" (the NumPy oracle on a bounded sample of the same
-workload, rank 0, N = 1 only).
+library's launches on its stream, during a profiled pass of the same steps),
+"cpu_baseline" (the NumPy oracle on a bounded sample of the same workload,
+rank 0, N = 1 only) and, at N = 1, "extra_workloads": the other BASELINE
+configurations this path runs on one GPU (configs[2] cvar/beta 0.3,
+configs[3] dynamic obstacles per GPU, configs[0] n = 50 / M = 2500), each
+with its own steps/s, median step and roofline.
 """
 from __future__ import annotations
 
@@ -40,66 +44,88 @@ for _p in (ROOT, PKG):
 kF = 22  # beta-CEM features per mother row (cx | cy)
 METRIC = "MPC optimizer steps/s (batch=1024,H=30,obs_samp=500) @1/2/4/8 GPU; % HBM roofline"
 
-# BASELINE.json configs[1] (headline), configs[2] and configs[3] (per GPU: one configuration per rank)
+# BASELINE.json configs[1] (headline), configs[2], configs[3] (per GPU: one configuration per rank), configs[0]
 WORKLOADS = {
     "mmd_opt": dict(desc="static obs, mmd_opt, batch=1024 rollouts, H=30, num_obs=10, obs_samples=484 (n=22, M=n^2)",
-                    cost="mmd_opt", num_reduced=22, num_obs=10, num_prime=30, noise="gaussian", level=0.1,
-                    num_batch=1024),
+                    baseline="configs[1]", cost="mmd_opt", num_reduced=22, num_obs=10, num_prime=30,
+                    noise="gaussian", level=0.1, num_batch=1024),
     "cvar": dict(desc="static obs, cvar, batch=1024 rollouts, H=30, num_obs=10, obs_samples=500, beta noise 0.3",
-                 cost="cvar", num_reduced=500, num_obs=10, num_prime=30, noise="beta", level=0.3,
-                 num_batch=1024),
+                 baseline="configs[2]", cost="cvar", num_reduced=500, num_obs=10, num_prime=30, noise="beta",
+                 level=0.3, num_batch=1024),
     "dynamic": dict(desc="dynamic obs, mmd_opt, batch=1024 rollouts, H=50, num_obs=20, obs_samples=1024 (n=32, M=n^2)",
-                    cost="mmd_opt", num_reduced=32, num_obs=20, num_prime=50, noise="gaussian", level=0.1,
-                    num_batch=1024, variant="dynamic"),
+                    baseline="configs[3] (per GPU)", cost="mmd_opt", num_reduced=32, num_obs=20, num_prime=50,
+                    noise="gaussian", level=0.1, num_batch=1024, variant="dynamic"),
+    "configs0": dict(desc="static obs, mmd_opt, num_batch=100 (reference), H=20, num_obs=4, num_reduced=50 (M=2500)",
+                     baseline="configs[0]", cost="mmd_opt", num_reduced=50, num_obs=4, num_prime=20,
+                     noise="gaussian", level=0.1, num_batch=100),
 }
 
-# MI355X peaks (MI355X_MICROARCH.md): fp32 vector 157.3 TFLOP/s = 78.6 T lane-ops/s
-# (one fp32 op per lane per cycle at full packing); HBM3E 8 TB/s
+# MI355X peaks (MI355X_MICROARCH.md): 1024 SIMDs at 2.4 GHz.  fp32 vector: one
+# lane-op per lane per cycle (32 lanes/cycle/SIMD) = 78.6 T lane-ops/s;
+# v_exp_f32 issues a wave64 instruction every 8 cycles (8 lanes/cycle/SIMD =
+# 19.7 T exp/s); fp64 vector 39.3 T lane-FMA/s; fp64 MFMA 78.6 TFLOP/s.
+SIMDS, CLOCK = 1024, 2.4e9
 VALU_PEAK_TOPS = 78.6
-VALU64_PEAK_TOPS = 39.3   # fp64 vector 78.6 TFLOP/s = 39.3 T lane-ops/s
+VALU64_PEAK_TOPS = 39.3
+MFMA64_PEAK_TFLOPS = 78.6
+# exp-term floor of k_bkernel: per summed term one v_exp_f32 (8 cycles / 64
+# lanes) + half a packed scale and half a packed add (2 cycles / 128 terms each)
+EXP_TERM_CYCLES = 8 / 64 + 2 / 128 + 2 / 128
+EXP_TERM_PEAK = SIMDS * CLOCK / EXP_TERM_CYCLES / 1e12   # 15.7 T terms/s
 HBM_PEAK_GBS = 8000.0
 
 
 def kernel_work(w, name, launches, stats):
-    """Algorithmic work of the profiled launches of kernel `name`, in fp32
-    lane-operations (DESIGN.md, Kernels):
-      bdist     per candidate and outer iteration: M x M distances x 22
-                features x 2 (sub, abs-add)
-      bkernel   per candidate and beta-iteration: the (sample, row) pairs
-                summed (counted by the kernel, stats[1]; 100 x n on the first
-                beta-iteration, 89 x n after) x (M exp terms + (n-1)/2 K_red
-                entries) x 3 (scale, exp, add)
-      risk_baseline  B x S rollouts x H steps x (bicycle step 40 + 9 per obstacle)
-    Returns (kind, ops) or None when no model is defined."""
+    """Algorithmic work of the profiled launches of kernel `name` (DESIGN.md
+    §4): (bound, unit, amount, peak).
+      bkernel  (sample, row) pairs summed (counted by the kernel, stats[1])
+               x (M exp terms + (n-1)/2 K_red entries), against the exp-term
+               issue floor (EXP_TERM_PEAK)
+      bsample  per candidate and beta-iteration, per 16-position block and 89
+               samples: T Z 16x16, U S 16x11, W^T Z 11x16 (2 flop each) +
+               W U^T 16x16x11, on fp64 MFMA
+      bqp      89 (n+1)-QPs per candidate: n^3/6 Cholesky + 2 n^2 solves + n^2
+               cost fp64 FMAs, against the fp64 vector FMA rate
+      bdist    M x M distances x 22 features x 2 (sub, abs-add) per candidate
+      beta_planes  B x S x H x 2 Beta draws x 37 fp64 lane-ops
+      risk_baseline  B x S rollouts x H steps x (bicycle 40 + 9 per obstacle (+ beta 320))"""
     B, H, O = w["num_batch"], w["num_prime"], w["num_obs"]
     n = w["num_reduced"]
     M = n * n
     if name == "bkernel":
-        # pairs summed (stats[1]) x (M exp terms + (n-1)/2 K_red entries on average) x 3 (scale, exp, add)
-        return "ops", stats[1] * (M + (n - 1) / 2) * 3
+        return "exp-issue", "T exp-terms/s", stats[1] * (M + (n - 1) / 2), EXP_TERM_PEAK
+    if name == "bsample":
+        nblk = (((M + 1) + 31) // 32) * 2
+        per = nblk * 89 * 2 * (16 * 16 + 16 * 11 + 11 * 16) + nblk * 16 * 16 * 11 * 2
+        return "mfma-fp64", "TFLOP/s", launches * B * per, MFMA64_PEAK_TFLOPS
+    if name == "bqp":
+        per = 89 * (n ** 3 / 6 + 3 * n * n)
+        return "valu-fp64", "T lane-FMA/s", launches * B * per, VALU64_PEAK_TOPS
     if name == "bdist":
-        return "ops", launches * B * M * M * kF * 2
+        return "valu", "T lane-ops/s", launches * B * M * M * kF * 2, VALU_PEAK_TOPS
     if name == "beta_planes":
-        # B x S x H x 2 Beta draws; per draw 2 gammas x (table transform 9 + log 1 + squeeze 5) + la/lb 4
-        # + exp 1 + ratio 2 = 37 fp64 lane-ops (a transcendental / divide / sqrt counted as 1)
-        return "ops64", launches * B * n * H * 2 * 37
+        return "valu-fp64", "T lane-ops/s", launches * B * n * H * 2 * 37, VALU64_PEAK_TOPS
     if name == "risk_baseline":
         beta = 2 * 160 if w["noise"] == "beta" else 0
-        return "ops", launches * B * n * H * (40 + O * 9 + beta)
+        return "valu", "T lane-ops/s", launches * B * n * H * (40 + O * 9 + beta), VALU_PEAK_TOPS
     return None
 
 
 def pmc_traffic(workload, kernel):
     """HBM bytes per launch of `kernel` in `workload` from the committed PMC
-    passes (profiles/r01_pmc_traffic.json, {workload: {kernel: bytes}}:
-    2 x FETCH_SIZE + WRITE_SIZE per the MI355X guide's gfx950 correction),
-    or None."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-    try:
-        with open(path) as f:
-            return json.load(f).get(workload, {}).get(kernel)
-    except (OSError, ValueError, AttributeError):
-        return None
+    passes (profiles/r02_pmc_traffic.json, else r01's; {workload: {kernel:
+    bytes}}: 2 x FETCH_SIZE + WRITE_SIZE per the MI355X guide's gfx950
+    correction), or None."""
+    for tag in ("r02", "r01"):
+        path = os.path.join(ROOT, "profiles", f"{tag}_pmc_traffic.json")
+        try:
+            with open(path) as f:
+                v = json.load(f).get(workload, {}).get(kernel)
+            if v is not None:
+                return v
+        except (OSError, ValueError, AttributeError):
+            continue
+    return None
 
 
 def make_workload(w, rank):
@@ -173,29 +199,13 @@ def cpu_baseline(w, inst, seconds):
                        f"({t_risk:.1f} s) scaled x{B / c:.1f}; BLAS threads {threads}")}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=40)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="mmd_opt", choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
-    ap.add_argument("--profile-steps", type=int, default=20)
-    a = ap.parse_args()
-
+def run_workload(name, steps, warmup, profile_steps, rank, world, local, dist=None):
+    """Time `steps` steps of workload `name` on this rank's GPU.  Returns the
+    timing record (rank-local elapsed time; the caller max-reduces it)."""
     import torch
-    import torch.distributed as dist
     from optimizer import _native
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world} (launch N>1 with torchrun)")
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    w = WORKLOADS[a.workload]
+    w = WORKLOADS[name]
     inst = make_workload(w, rank)
     T = 20
     cfg = _native.make_config(w["num_reduced"], w["num_obs"], w["level"], w["num_prime"], w["noise"], 0.0, 0.0,
@@ -205,44 +215,87 @@ def main():
     stream = torch.cuda.current_stream()
     h.set_stream(stream.cuda_stream)
 
-    def run(k0, count):
+    def run(k0, count, evs=None):
         for i in range(k0, k0 + count):
             t = i % T
             if t == 0:
                 h.begin(w["cost"], inst["idx_mpc"], inst["init"], inst["mean"], inst["cov"], inst["xo"], inst["yo"],
                         inst["v_des"])
             h.iterate(t, 1)
+            if evs is not None:
+                evs[i - k0 + 1].record(stream)
 
-    run(0, a.warmup)
+    run(0, warmup)
     h.sync()
     torch.cuda.synchronize()
-    # timed region: K steps, fresh solve boundaries every 20 steps
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     t0 = time.perf_counter()
-    ev0.record(stream)
-    run(0, a.steps)
-    ev1.record(stream)
+    evs[0].record(stream)
+    run(0, steps, evs)
     h.sync()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    ev_ms = ev0.elapsed_time(ev1)
+    step_ms = np.array([evs[i].elapsed_time(evs[i + 1]) for i in range(steps)])
+    res = h.finish()
+    # profiled pass (same steps, HIP events around every launch on the library's stream)
+    h.write("stats", np.zeros(8, np.uint64))
+    h.profile(True)
+    run(0, profile_steps)
+    h.sync()
+    kt = h.kernel_times()
+    h.profile(False)
+    stats = h.read("stats", np.uint64).astype(np.int64)
+    h.close()
+    busy = {k: v for k, v in kt.items() if v[0] > 0}
+    dom = max(busy, key=lambda k: busy[k][1])
+    launches, tot_ms = busy[dom]
+    avg_s = tot_ms / launches / 1e3
+    roof = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None}
+    model = kernel_work(w, dom, launches, stats)
+    if model is not None:
+        bound, unit, amount, peak = model
+        roof.update(bound=bound, unit=unit, peak=peak, achieved=amount / launches / avg_s / 1e12)
+        roof["frac"] = roof["achieved"] / peak
+    roof["traffic"] = pmc_traffic(name, dom)
+    roof["kernel"] = dom
+    roof["avg_us"] = avg_s * 1e6
+    return dict(w=w, elapsed=elapsed, step_ms=step_ms, res=res, roof=roof, inst=inst,
+                kernels={k: v[1] / profile_steps for k, v in busy.items()})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="mmd_opt", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--profile-steps", type=int, default=20)
+    ap.add_argument("--extra", type=int, default=1, help="N = 1: also time the other BASELINE workloads (0 = skip)")
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world} (launch N>1 with torchrun)")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    r = run_workload(a.workload, a.steps, a.warmup, a.profile_steps, rank, world, local, dist if world > 1 else None)
+    elapsed = r["elapsed"]
+    res = r["res"]
     if world > 1:
         el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         elapsed = float(el.item())
         dist.barrier()
-    res = h.finish()
-    # profiled pass (same steps, HIP events around every launch on the library's stream)
-    h.write("stats", np.zeros(8, np.uint64))
-    h.profile(True)
-    run(0, a.profile_steps)
-    h.sync()
-    kt = h.kernel_times()
-    h.profile(False)
-    stats = h.read("stats", np.uint64).astype(np.int64)
     # final gather of per-config results over RCCL (§8e)
     vec = np.concatenate([res["cx"], res["cy"], [res["cost_lane"], res["cost_obs"]]]).astype(np.float32)
     if world > 1:
@@ -253,41 +306,41 @@ def main():
     else:
         gathered = vec[None]
     if rank == 0:
-        steps_total = a.steps * world
-        value = steps_total / elapsed
-        busy = {k: v for k, v in kt.items() if v[0] > 0}
-        dom = max(busy, key=lambda k: busy[k][1])
-        launches, tot_ms = busy[dom]
-        avg_s = tot_ms / launches / 1e3
-        model = kernel_work(w, dom, launches, stats)
-        peak = VALU64_PEAK_TOPS if model is not None and model[0] == "ops64" else VALU_PEAK_TOPS
-        roof = {"bound": "valu", "achieved": None, "peak": peak, "unit": "Tops/s", "frac": None}
-        if model is not None:
-            roof["achieved"] = model[1] / launches / avg_s / 1e12
-            roof["frac"] = roof["achieved"] / peak
-            if model[0] == "ops64":
-                roof["bound"] = "valu-fp64"
-        roof["traffic"] = pmc_traffic(a.workload, dom)
-        roof["kernel"] = dom
-        roof["avg_us"] = avg_s * 1e6
+        w = r["w"]
+        T = 20
+        value = a.steps * world / elapsed
         line = {
             "metric": METRIC, "value": value, "unit": "steps/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": f"synthetic ({w.get('variant', 'static')} obstacle configs k=rank, internal Philox noise)",
-            "config": {"workload": w["desc"], "cost": w["cost"], "global_batch": w["num_batch"] * world,
-                       "num_batch": w["num_batch"], "num_prime": w["num_prime"], "num_obs": w["num_obs"],
-                       "num_reduced": w["num_reduced"], "noise": w["noise"], "noise_level": w["level"],
-                       "parallelism": f"config-sharded x{world}", "solves_per_s": value / T},
-            "roofline": roof,
-            "kernels_ms_per_step": {k: v[1] / a.profile_steps for k, v in busy.items()},
-            "event_ms_rank0": ev_ms,
+            "config": {"workload": w["desc"], "baseline": w["baseline"], "cost": w["cost"],
+                       "global_batch": w["num_batch"] * world, "num_batch": w["num_batch"],
+                       "num_prime": w["num_prime"], "num_obs": w["num_obs"], "num_reduced": w["num_reduced"],
+                       "noise": w["noise"], "noise_level": w["level"], "parallelism": f"config-sharded x{world}",
+                       "solves_per_s": value / T},
+            "median_ms_per_step": float(np.median(r["step_ms"])),
+            "roofline": r["roof"],
+            "kernels_ms_per_step": r["kernels"],
             "results_gathered": int(gathered.shape[0]),
         }
         if world == 1 and a.cpu_seconds > 0:
-            line["cpu_baseline"] = cpu_baseline(w, inst, a.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(w, r["inst"], a.cpu_seconds)
+        if world == 1 and a.extra:
+            extra = {}
+            for name in WORKLOADS:
+                if name == a.workload:
+                    continue
+                steps = max(20, a.steps // (5 if name == "configs0" else 1))
+                x = run_workload(name, steps, 2, 20, rank, 1, local)
+                extra[name] = {"baseline": x["w"]["baseline"], "workload": x["w"]["desc"],
+                               "value": steps / x["elapsed"], "unit": "steps/s", "steps": steps,
+                               "ms_per_step": x["elapsed"] / steps * 1e3,
+                               "median_ms_per_step": float(np.median(x["step_ms"])),
+                               "solves_per_s": steps / x["elapsed"] / T, "roofline": x["roof"],
+                               "kernels_ms_per_step": x["kernels"]}
+            line["extra_workloads"] = extra
         print(json.dumps(line), flush=True)
-    h.close()
     if world > 1:
         dist.destroy_process_group()
 
