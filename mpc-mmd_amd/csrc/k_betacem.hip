@@ -748,18 +748,33 @@ DEVI void bqp_quad(const Params& p, int tb) {
   // own rows: A[t][k] = C[4t+q][k], k <= 4t+3 (k > row: 0)
   double A[T4][NP];
   double g[T4], a1[T4], a2[T4], rin[T4];
+  // every load unconditional (clamped address, value masked afterwards) so
+  // they are all in flight together: one memory latency, not one per entry
+  float kv[T4][NP];
+  double bv[T4];
+#pragma unroll
+  for (int t = 0; t < T4; ++t) {
+    const int i = 4 * t + q;
+    const int ic = min(i, n - 1);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      if (k > 4 * t + 3) continue;
+      const int e = ic > 0 ? ic * (ic - 1) / 2 + max(min(k, ic - 1), 0) : 0;  // always a valid entry (n >= 2)
+      kv[t][k] = kr[e];
+    }
+    bv[t] = br[ic];
+  }
 #pragma unroll
   for (int t = 0; t < T4; ++t) {
     const int i = 4 * t + q;
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       if (k > 4 * t + 3) continue;
-      double v = 0.0;
-      if (k < i && i < n) v = double(kr[i * (i - 1) / 2 + k]);
+      double v = (k < i && i < n) ? double(kv[t][k]) : 0.0;
       if (k == i) v = i < n ? cdiag : 1.0;
       A[t][k] = v;
     }
-    g[t] = i < n ? br[i] * inv_m : 0.0;
+    g[t] = i < n ? bv[t] * inv_m : 0.0;
     a1[t] = g[t];
     a2[t] = i < n ? 1.0 : 0.0;
     rin[t] = 0.0;
@@ -905,14 +920,20 @@ __global__ __launch_bounds__(256) void k_bqp_wave(Params p, int tb) {
   const double cdiag = double(1.0f + 0.05f);
   const bool real = lane < n;
   double A[NP];
+  const int ic = min(lane, n - 1);
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {  // unconditional loads (clamped entry), masked after
+    const int e = ic > 0 ? ic * (ic - 1) / 2 + max(min(k, ic - 1), 0) : 0;
+    A[k] = double(kr[e]);
+  }
+  const double brv = br[ic];
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
-    double v = 0.0;
-    if (k < lane && real) v = double(kr[lane * (lane - 1) / 2 + k]);
+    double v = (k < lane && real) ? A[k] : 0.0;
     if (k == lane) v = real ? cdiag : 1.0;
     A[k] = v;
   }
-  const double g = real ? br[lane] * inv_m : 0.0;
+  const double g = real ? brv * inv_m : 0.0;
   double rdiag = 1.0;
   // Cholesky, column j
 #pragma unroll
@@ -1063,19 +1084,25 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
     {
       float v[kBetaElite];
       double s = 0.0;
+      const int jc = min(j, M);
+      // the 11 loads are unconditional (clamped position, source row chosen
+      // by pointer) so they are in flight together
 #pragma unroll
       for (int q = 0; q < kBetaElite; ++q) {
         const int e = elite[q];
-        float x = 0.0f;
+        const float* src = tb == 0 ? p.beta_z0 + size_t(e) * M1
+                                   : (e < kBetaElite ? Eold + size_t(e) * M1 : Y + size_t(e - kBetaElite) * ys);
+        v[q] = src[jc];
+      }
+#pragma unroll
+      for (int q = 0; q < kBetaElite; ++q) {
+        float x = v[q];
+        if (tb == 0) {
+          x = float(kSqrt20 * double(x));
+          if (j == M) x = fmaxf(x, 0.01f);
+        }
+        x = valid ? x : 0.0f;
         if (valid) {
-          if (tb == 0) {
-            x = float(kSqrt20 * double(p.beta_z0[size_t(e) * M1 + j]));
-            if (j == M) x = fmaxf(x, 0.01f);
-          } else if (e < kBetaElite) {
-            x = Eold[size_t(e) * M1 + j];
-          } else {
-            x = Y[size_t(e - kBetaElite) * ys + j];
-          }
           Enew[size_t(q) * M1 + j] = x;
           if (j == M) sig_new[q] = x;
         }
