@@ -361,7 +361,10 @@ DEVI void select_batch(Row row, Out out, int first, int last, int stride, int M,
 //   A: A[r][h]   B: B[h][r]   C/D register i: C[h + 4 i][r]
 typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int kSampleTiles = kBzCols / 16;  // 6 tiles of 16 sample columns (89 used)
-constexpr int kTilesPerWave = 6;
+#ifndef MPCMMD_SAMPLE_TILES
+#define MPCMMD_SAMPLE_TILES 6
+#endif
+constexpr int kTilesPerWave = MPCMMD_SAMPLE_TILES;
 constexpr int kSampleWaves = kSampleTiles / kTilesPerWave;
 static_assert(kSampleTiles % kTilesPerWave == 0, "tiles per wave");
 static_assert(kBzCols >= kNew, "sample tiles");
@@ -1161,77 +1164,83 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
   }
 }
 
-// k_bgen: level 2 of the generators, one thread per position j (no
-// cross-thread dependency): Phi_j = the block prefix (k_belite) + the
-// rank-1 terms of the earlier positions of j's block, its Cholesky,
-// v = Phi_j^-1 u_j, L_jj = sqrt(0.05 + u_j . v), w_j = v / L_jj.
-// Separate from k_belite so that kernel's LDS-bound phases are not held to
-// this phase's register count (184 VGPRs).
+// k_bgen: level 2 of the generators, one thread per (candidate, block of 16
+// positions).  The block prefix Phi_b (k_belite) is factored once and
+// inverted, A = Phi_b^-1; then, position by position through the block,
+//   v_j = A u_j,  L_jj = sqrt(0.05 + u_j . v_j),  w_j = v_j / L_jj,
+//   A <- A - w_j w_j^T      (= Phi_{j+1}^-1: Sherman-Morrison, since
+//                            Phi_{j+1} = Phi_j + u_j u_j^T / 0.05)
+// -- at most 15 rank-1 steps from an exactly factored start, so the error
+// stays at the level of one fp64 Cholesky.  Each block is a short sequential
+// chain; the ~32 blocks per candidate run in parallel.
+HDI int sym11i(int a, int c) { return a <= c ? sym11(a, c) : sym11(c, a); }
+
 __global__ __launch_bounds__(64) void k_bgen(Params p) {
-  __shared__ double us[64 * 11];  // u of this workgroup's 64 positions (whole 16-blocks)
-  const int b = p.b0 + blockIdx.y, M = p.M, M1 = M + 1;
-  const int j0 = blockIdx.x * 64, j = j0 + threadIdx.x;
-  const int nblk = (M1 + 15) / 16;
+  const int M = p.M, M1 = M + 1, nblk = (M1 + 15) / 16;
+  const int gid = blockIdx.x * 64 + threadIdx.x;
+  if (gid >= p.nb * nblk) return;
+  const int b = p.b0 + gid / nblk, blk = gid % nblk;
   double* gen = p.gen + size_t(b) * pos_pad(M) * kGenStride;
-  const double* Gb = p.phib + size_t(b) * nblk * 66;
-  for (int i = threadIdx.x; i < 64 * 11; i += 64) {
-    const int r = i / 11, a = i - r * 11;
-    us[i] = j0 + r < M1 ? gen[size_t(j0 + r) * kGenStride + kGenU + a] : 0.0;
+  const double* Gb = p.phib + (size_t(b) * nblk + blk) * 66;
+  double A[66];
+#pragma unroll
+  for (int e = 0; e < 66; ++e) A[e] = Gb[e];
+  // Cholesky Phi_b = R^T R (R upper, in A; rinv = 1 / diag)
+  double rinv[11];
+#pragma unroll
+  for (int a = 0; a < 11; ++a) {
+    double d = A[sym11(a, a)];
+#pragma unroll
+    for (int k = 0; k < a; ++k) d = fma(-A[sym11(k, a)], A[sym11(k, a)], d);
+    d = sqrt(d);
+    A[sym11(a, a)] = d;
+    rinv[a] = 1.0 / d;
+#pragma unroll
+    for (int c = a + 1; c < 11; ++c) {
+      double s = A[sym11(a, c)];
+#pragma unroll
+      for (int k = 0; k < a; ++k) s = fma(-A[sym11(k, a)], A[sym11(k, c)], s);
+      A[sym11(a, c)] = s * rinv[a];
+    }
   }
-  __syncthreads();
-  if (j >= M1) return;
-  {
-    const int blk = j >> 4;
-    double A[66];
+  // X = R^-1 (upper), column by column: X_cc = 1 / R_cc, X_ac = -(sum_{a<k<=c} R_ak X_kc) / R_aa
+  double X[66];
 #pragma unroll
-    for (int e = 0; e < 66; ++e) A[e] = Gb[blk * 66 + e];
-    for (int k = blk * 16; k < j; ++k) {
-      double uk[11];
+  for (int c = 0; c < 11; ++c) {
+    X[sym11(c, c)] = rinv[c];
 #pragma unroll
-      for (int a = 0; a < 11; ++a) uk[a] = us[(k - j0) * 11 + a];
+    for (int a = c - 1; a >= 0; --a) {
+      double s = 0.0;
 #pragma unroll
-      for (int a = 0; a < 11; ++a) {
-        const double ua = uk[a] * kInvRidge;
-#pragma unroll
-        for (int c = a; c < 11; ++c) A[sym11(a, c)] = fma(ua, uk[c], A[sym11(a, c)]);
-      }
+      for (int k = a + 1; k <= c; ++k) s = fma(A[sym11(a, k)], X[sym11(k, c)], s);
+      X[sym11(a, c)] = -s * rinv[a];
     }
-    // Cholesky A = R^T R (R upper, stored in A; rinv = 1 / diag)
-    double rinv[11];
+  }
+  // A = Phi_b^-1 = X X^T (symmetric, packed upper)
+#pragma unroll
+  for (int a = 0; a < 11; ++a)
+#pragma unroll
+    for (int c = a; c < 11; ++c) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = c; k < 11; ++k) s = fma(X[sym11(a, k)], X[sym11(c, k)], s);
+      A[sym11(a, c)] = s;
+    }
+  const int j0 = blk * 16, j1 = min(M1, j0 + 16);
+  double u[11], un[11];
+#pragma unroll
+  for (int a = 0; a < 11; ++a) u[a] = gen[size_t(j0) * kGenStride + kGenU + a];
+  for (int j = j0; j < j1; ++j) {
+    const int jn = min(j + 1, j1 - 1);  // the next position's u in flight meanwhile
+#pragma unroll
+    for (int a = 0; a < 11; ++a) un[a] = gen[size_t(jn) * kGenStride + kGenU + a];
+    double v[11];
 #pragma unroll
     for (int a = 0; a < 11; ++a) {
-      double d = A[sym11(a, a)];
+      double s = 0.0;
 #pragma unroll
-      for (int k = 0; k < a; ++k) d = fma(-A[sym11(k, a)], A[sym11(k, a)], d);
-      d = sqrt(d);
-      A[sym11(a, a)] = d;
-      rinv[a] = 1.0 / d;
-#pragma unroll
-      for (int c = a + 1; c < 11; ++c) {
-        double s = A[sym11(a, c)];
-#pragma unroll
-        for (int k = 0; k < a; ++k) s = fma(-A[sym11(k, a)], A[sym11(k, c)], s);
-        A[sym11(a, c)] = s * rinv[a];
-      }
-    }
-    double u[11], v[11];
-#pragma unroll
-    for (int a = 0; a < 11; ++a) u[a] = us[threadIdx.x * 11 + a];
-    // R^T y = u
-#pragma unroll
-    for (int a = 0; a < 11; ++a) {
-      double s = u[a];
-#pragma unroll
-      for (int k = 0; k < a; ++k) s = fma(-A[sym11(k, a)], v[k], s);
-      v[a] = s * rinv[a];
-    }
-    // R v = y
-#pragma unroll
-    for (int a = 10; a >= 0; --a) {
-      double s = v[a];
-#pragma unroll
-      for (int k = a + 1; k < 11; ++k) s = fma(-A[sym11(a, k)], v[k], s);
-      v[a] = s * rinv[a];
+      for (int c = 0; c < 11; ++c) s = fma(A[sym11i(a, c)], u[c], s);
+      v[a] = s;
     }
     double uv = 0.0;
 #pragma unroll
@@ -1239,9 +1248,19 @@ __global__ __launch_bounds__(64) void k_bgen(Params p) {
     const double ljj = sqrt(kRidge + uv);
     const double rl = 1.0 / ljj;
     double* g = gen + size_t(j) * kGenStride;
+    double w[11];
 #pragma unroll
-    for (int a = 0; a < 11; ++a) g[kGenW + a] = v[a] * rl;
+    for (int a = 0; a < 11; ++a) {
+      w[a] = v[a] * rl;
+      g[kGenW + a] = w[a];
+    }
     g[kGenL] = ljj;
+#pragma unroll
+    for (int a = 0; a < 11; ++a)
+#pragma unroll
+      for (int c = a; c < 11; ++c) A[sym11(a, c)] = fma(-w[a], w[c], A[sym11(a, c)]);
+#pragma unroll
+    for (int a = 0; a < 11; ++a) u[a] = un[a];
   }
 }
 
@@ -1446,7 +1465,11 @@ void launch_bkernel(const Params& p, int tb, hipStream_t s) {
 void launch_belite(const Params& p, int tb, hipStream_t s) {
   const EliteLds e = elite_lds(p.M + 1);
   hipLaunchKernelGGL(k_belite, dim3(p.nb), dim3(kThreads), e.total, s, p, tb);
-  hipLaunchKernelGGL(k_bgen, dim3((p.M + 1 + 63) / 64, p.nb), dim3(64), 0, s, p);
+}
+
+void launch_bgen(const Params& p, int tb, hipStream_t s) {
+  const int nblk = (p.M + 1 + 15) / 16;
+  hipLaunchKernelGGL(k_bgen, dim3((p.nb * nblk + 63) / 64), dim3(64), 0, s, p);
   if (tb == kBetaIters - 1) hipLaunchKernelGGL(k_bsigma, dim3(p.nb), dim3(kThreads), 0, s, p, tb);
 }
 

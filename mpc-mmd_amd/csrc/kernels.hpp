@@ -193,6 +193,7 @@ void launch_bselect(const Params& p, int tb, hipStream_t s);
 void launch_bkernel(const Params& p, int tb, hipStream_t s);
 void launch_bqp(const Params& p, int tb, hipStream_t s);
 void launch_belite(const Params& p, int tb, hipStream_t s);
+void launch_bgen(const Params& p, int tb, hipStream_t s);  // + k_bsigma on the last beta-iteration
 void launch_mmdfinal(const Params& p, int t, hipStream_t s);
 bool mmdopt_supported(int n, int H, int O, std::string* why);
 }  // namespace mpcmmd

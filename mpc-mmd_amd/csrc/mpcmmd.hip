@@ -57,11 +57,12 @@ enum KernelId {
   kKSelect,
   kKGammaTab,
   kKBetaPlanes,
+  kKBGen,
   kNumKernels
 };
 const char* kKernelNames[kNumKernels] = {"noise",   "front", "risk_baseline", "mother",   "bdist", "bsample",
                                          "bselect", "bkernel", "bqp",         "belite", "mmdfinal", "select",
-                                         "gamma_tab", "beta_planes"};
+                                         "gamma_tab", "beta_planes", "bgen"};
 
 }  // namespace
 
@@ -239,6 +240,7 @@ void run_beta_iteration(mpcmmd_handle* h, const Params& p, int tb, hipStream_t s
   h->launch(kKBKernel, [&] { launch_bkernel(p, tb, st); });
   h->launch(kKBQp, [&] { launch_bqp(p, tb, st); });
   h->launch(kKBElite, [&] { launch_belite(p, tb, st); });
+  h->launch(kKBGen, [&] { launch_bgen(p, tb, st); });
 }
 
 // the 20 beta-CEM iterations of every candidate: one chain per candidate
@@ -313,7 +315,10 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
         h->launch(kKBKernel, [&] { launch_bkernel(p, t, h->stream); });
         h->launch(kKBQp, [&] { launch_bqp(p, t, h->stream); });
       }
-      if (stage == 7) h->launch(kKBElite, [&] { launch_belite(p, t, h->stream); });
+      if (stage == 7) {
+        h->launch(kKBElite, [&] { launch_belite(p, t, h->stream); });
+        h->launch(kKBGen, [&] { launch_bgen(p, t, h->stream); });
+      }
       if (stage == 8) h->launch(kKMmdFinal, [&] { launch_mmdfinal(p, t, h->stream); });
       break;
     default:
