@@ -30,6 +30,8 @@
 // v_j = Phi_j^-1 u_j, L_jj = sqrt(d + u_j.v_j), w_j = v_j / L_jj, one has
 // L_ij = u_i . w_j (i > j), so (L z)_i = L_ii z_i + u_i . sum_{j<i} w_j z_j.
 // Same factor as chol(cov) in exact arithmetic, O(M r^2) instead of O(M^3).
+#include <cstdlib>
+
 #include "block.hpp"
 #include "kernels.hpp"
 #include "rng.hpp"
@@ -518,28 +520,44 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
 }
 
 // ------------------------------------------------------------------------
-// k_bkernel: one workgroup (1024 threads) per candidate.
+// k_bkernel: kernel_computation.py:19-65 / compute_beta.py:120-127 for every
+// sample of the iteration.  Workgroup = (candidate, part); a candidate's
+// distinct rows are split over `split` parts when the batch alone cannot
+// fill the chip.
 //
-//   rows     the distinct mother rows the samples selected (union U, ~150 of
-//            484 at n = 22); each is a row of the distance matrix k_bdist
-//            wrote this outer iteration (kernel_computation.py:33-39), staged
-//            into LDS by LDS-DMA, chunk c + 1 in flight while chunk c is
-//            summed (two buffers)
-//   pairs    (sample, reduced row) pairs sorted by row; an 8-lane group sums
-//            exp(-D[r][j] / sigma_s) over j (v_exp_f32 on d * (-log2 e /
-//            sigma), packed scale / add), and writes the sample's K_red
-//            entries of that row
+//   pairs    (sample s, reduced position k) of this iteration's selections,
+//            counting-sorted by their mother row r = sel[s][k] (LDS), and
+//            the list of the distinct rows (~150 of 484 at n = 22)
+//   rows     a wave takes the next distinct row (LDS counter) and holds its
+//            distance-matrix row (k_bdist, kernel_computation.py:33-39) in
+//            registers (lane L: float4s L + 64 t); for small rows the next
+//            row's loads are issued before the current one is summed.  The
+//            row's pairs are summed 8 at a time: per lane and pair the
+//            lane's terms exp2(D[r][j] * (-log2 e / sigma_s)) (v_exp_f32,
+//            packed scale / add), then one transposing cross-lane reduction
+//            (permlane32 / permlane16 swaps, DPP) leaves pair j's row sum in
+//            lane 8 j + 4
+//   K_red    the batch's entries exp(-D[r][sel[s][kk]] / sigma_s), kk < k
+//            (8 lanes per pair), gathered from a wave-private LDS copy of the row
+// No D row is staged through a shared buffer, so there are no barriers after
+// the setup and no chunk quantisation: every exp is one of the M terms of a
+// real pair (plus the row padding to whole 256-column blocks).
 // From the second beta-iteration on, samples 0..10 are the previous elites:
 // their selection, kernels and QP are unchanged, k_belite carried them, and
 // only samples 11..99 are processed here.
-constexpr int kKerThreads = 1024;
+#ifndef MPCMMD_KER_WAVES
+#define MPCMMD_KER_WAVES 16
+#endif
+constexpr int kKerWavesMax = MPCMMD_KER_WAVES;
 
 struct KerLds {
-  size_t sel, csg, cnt, fill, start, ulist, urank, pairs, pair_s, work, total;
-  int rows;  // D rows per buffer (two buffers)
+  size_t sel, csg, pairs, ulist, ustart, misc, rowbuf, total;
 };
 
-HDI KerLds ker_lds(int M, int n, size_t budget) {
+// persistent: sel (short), csg, pairs (K_red offset | k << 18 | s << 24), the distinct rows
+// and their first pair; the setup's counts / fill / scan (10 M bytes) overlay
+// the wave row buffers
+HDI KerLds ker_lds(int M, int n, int waves) {
   KerLds L{};
   size_t o = 0;
   auto take = [&](size_t bytes) {
@@ -547,161 +565,254 @@ HDI KerLds ker_lds(int M, int n, size_t budget) {
     o = (o + bytes + 15) & ~size_t(15);
     return at;
   };
-  L.sel = take(size_t(kBetaSamples) * n * 2);    // short
+  L.sel = take(size_t(kBetaSamples) * n * 2);
   L.csg = take(size_t(kBetaSamples) * 4);
-  L.cnt = take(size_t(M) * 4);                   // int (LDS atomics)
-  L.fill = take(size_t(M) * 4);
-  L.start = take(size_t(M) * 2);                 // ushort: <= 100 n
+  L.pairs = take(size_t(kBetaSamples) * n * 4);
   L.ulist = take(size_t(M) * 2);
-  L.urank = take(size_t(M) * 2);
-  L.pairs = take(size_t(kBetaSamples) * n * 2);
-  L.pair_s = take(size_t(kBetaSamples) * n);
-  L.work = o;
-  const size_t rest = budget > o ? budget - o : 0;
-  int rows = int(rest / (size_t(2) * dist_stride(M) * 4));
-  if (rows > 128) rows = 128;
-  L.rows = rows;
-  L.total = o + size_t(2) * rows * dist_stride(M) * 4;
+  L.ustart = take(size_t(M + 1) * 2);
+  L.misc = take(32 * 4);  // [0] next row, [1] distinct rows, [16..31] scan wave totals
+  const size_t rb = size_t(waves) * dist_stride(M) * 4, setup = size_t(M) * 10;
+  L.rowbuf = take(rb > setup ? rb : setup);
+  L.total = o;
   return L;
 }
 
 constexpr size_t kLdsBudget = 160 * 1024 - 1024;
-// k_bkernel runs two workgroups per CU (one's D-row loads overlap the
-// other's exp sums) whenever half the LDS still holds this many D rows per buffer
-constexpr size_t kKerHalfBudget = 80 * 1024;
-constexpr int kKerMinRowsHalf = 4;
+// waves per workgroup: 16 (one workgroup per candidate and half a CU) while
+// the row buffers leave room for two workgroups per CU
+int ker_waves(int M, int n) {
+  int wv = kKerWavesMax;
+  while (wv > 4 && ker_lds(M, n, wv).total > 80 * 1024) wv >>= 1;
+  return wv;
+}
+
 constexpr float kNegLog2e = -1.44269504088896340736f;
 
-__global__ __launch_bounds__(kKerThreads) void k_bkernel(Params p, int tb, int budget) {
+DEVI float dpp_f_ror8(float v) { return __int_as_float(dpp_i<0x128>(__float_as_int(v))); }
+
+// v_permlane32_swap (W = 32): lanes 32-63 of x <-> lanes 0-31 of y;
+// v_permlane16_swap (W = 16): the odd 16-lane rows of x <-> the even rows of y.
+// Inline asm: hipcc (ROCm 7.2) may commute the builtins' two operands, which
+// exchanges the other halves.  s_nop 1: the VALU-write -> permlane hazard.
+template <int W>
+DEVI void permlane_swap(float& x, float& y) {
+  if constexpr (W == 32)
+    __asm__ volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+  else
+    __asm__ volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+
+// v[j] per lane -> lanes 8 j + 4..7 hold the 64-lane sum of v[j] (row_ror:4
+// moves lane i - 4 into lane i, so the 8-lane group's total lands in its upper quad)
+DEVI float transpose_sum8(const float (&v)[8]) {
+  const int lane = threadIdx.x & 63;
+  float a[4], c2[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // lanes 0-31: slots 0..3, lanes 32-63: slots 4..7
+    float x = v[i], y = v[4 + i];
+    permlane_swap<32>(x, y);
+    a[i] = x + y;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // lane bit 4 picks slot 4 h + 2 b4 + i
+    float x = a[i], y = a[2 + i];
+    permlane_swap<16>(x, y);
+    c2[i] = x + y;
+  }
+  const bool b3 = lane & 8;  // lane bit 3 picks slot 4 h + 2 b4 + b3 = lane >> 3
+  const float y0 = dpp_f_ror8(c2[0]), y1 = dpp_f_ror8(c2[1]);
+  float x = b3 ? c2[1] + y1 : c2[0] + y0;
+  x += __int_as_float(dpp_i<0xB1>(__float_as_int(x)));
+  x += __int_as_float(dpp_i<0x4E>(__float_as_int(x)));
+  return x + __int_as_float(dpp_i<0x124>(__float_as_int(x)));
+}
+
+template <int NV4>
+__global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb, int split) {
+  constexpr bool kPrefetch = NV4 <= 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int b = p.b0 + blockIdx.x, M = p.M, n = p.n, Md = dist_stride(M);
+  const int waves = blockDim.x >> 6;
+  const int cand = blockIdx.x / split, part = blockIdx.x - cand * split;
+  const int b = p.b0 + cand, M = p.M, n = p.n, Md = dist_stride(M);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const KerLds C = ker_lds(M, n, size_t(budget));
+  const KerLds C = ker_lds(M, n, waves);
   short* sl = reinterpret_cast<short*>(smem + C.sel);
   float* csg = reinterpret_cast<float*>(smem + C.csg);
-  double* rowsum = p.brow + size_t(b) * kBetaSamples * n;
-  int* cnt = reinterpret_cast<int*>(smem + C.cnt);
-  int* fill = reinterpret_cast<int*>(smem + C.fill);
-  unsigned short* start = reinterpret_cast<unsigned short*>(smem + C.start);
+  uint32_t* pairs = reinterpret_cast<uint32_t*>(smem + C.pairs);
   unsigned short* ulist = reinterpret_cast<unsigned short*>(smem + C.ulist);
-  unsigned short* urank = reinterpret_cast<unsigned short*>(smem + C.urank);
-  short* pairs = reinterpret_cast<short*>(smem + C.pairs);
-  unsigned char* pair_s = reinterpret_cast<unsigned char*>(smem + C.pair_s);
-  float* Dl = reinterpret_cast<float*>(smem + C.work);
+  unsigned short* ustart = reinterpret_cast<unsigned short*>(smem + C.ustart);
+  int* misc = reinterpret_cast<int*>(smem + C.misc);  // [0] next row, [1] distinct rows
+  int* cnt = reinterpret_cast<int*>(smem + C.rowbuf);  // setup only
+  int* fill = cnt + M;
+  unsigned short* start = reinterpret_cast<unsigned short*>(fill + M);
+  double* rowsum = p.brow + size_t(b) * kBetaSamples * n;
+  const int ntri = n * (n - 1) / 2;
   const int s_lo = first_sample(tb);
   const int i_lo = s_lo * n, i_hi = kBetaSamples * n;
   MPCMMD_STAMP(p, 16);
+#ifdef MPCMMD_WGT
+  if (tid == 0) p.wgt[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
   const int32_t* gsel = p.bsel + size_t(b) * kBetaSamples * n;
-  for (int i = i_lo + tid; i < i_hi; i += kKerThreads) sl[i] = short(gsel[i]);
-  for (int s = s_lo + tid; s < kBetaSamples; s += kKerThreads)
+  for (int i = i_lo + tid; i < i_hi; i += blockDim.x) sl[i] = short(gsel[i]);
+  for (int s = s_lo + tid; s < kBetaSamples; s += blockDim.x)
     csg[s] = kNegLog2e / p.bsig[size_t(b) * kBetaSamples + s];
-  for (int r = tid; r < M; r += kKerThreads) {
+  for (int r = tid; r < M; r += blockDim.x) {
     cnt[r] = 0;
     fill[r] = 0;
   }
+  if (tid == 0) misc[0] = 0;
   __syncthreads();
-  for (int i = i_lo + tid; i < i_hi; i += kKerThreads) atomicAdd(&cnt[sl[i]], 1);
+  for (int i = i_lo + tid; i < i_hi; i += blockDim.x) atomicAdd(&cnt[sl[i]], 1);
   __syncthreads();
-  if (w == 0) {  // exclusive scans of cnt and (cnt > 0), one wave
-    const int per = (M + 63) / 64, a = lane * per, e = min(M, a + per);
-    int s1 = 0, s2 = 0;
+  {  // exclusive scans of cnt and (cnt > 0), packed as cnt | (cnt > 0) << 16
+     // (totals <= 6400 pairs, <= 4096 rows): thread runs, wave scans, wave totals
+    const int nt = blockDim.x, per = (M + nt - 1) / nt, a = tid * per, e = min(M, a + per);
+    int sp = 0;
     for (int r = a; r < e; ++r) {
-      s1 += cnt[r];
-      s2 += cnt[r] > 0;
+      const int c = cnt[r];
+      sp += c | (c > 0) << 16;
     }
-    int x1 = s1, x2 = s2;
+    int x = sp;
+#pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-      const int y1 = __shfl_up(x1, o, 64), y2 = __shfl_up(x2, o, 64);
-      if (lane >= o) {
-        x1 += y1;
-        x2 += y2;
-      }
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
     }
-    x1 -= s1;
-    x2 -= s2;
+    if (lane == 63) misc[16 + w] = x;
+    __syncthreads();
+    int base = 0;
+    for (int v = 0; v < w; ++v) base += misc[16 + v];
+    x += base - sp;  // exclusive prefix of this thread's run
+    if (tid == nt - 1) {
+      const int tot = x + sp;
+      misc[1] = tot >> 16;
+      ustart[tot >> 16] = (unsigned short)(tot & 0xFFFF);
+    }
     for (int r = a; r < e; ++r) {
+      const int c = cnt[r], x1 = x & 0xFFFF, x2 = x >> 16;
       start[r] = (unsigned short)x1;
-      urank[r] = (unsigned short)x2;
-      if (cnt[r] > 0) ulist[x2] = (unsigned short)r;
-      x1 += cnt[r];
-      x2 += cnt[r] > 0;
+      if (c > 0) {
+        ulist[x2] = (unsigned short)r;
+        ustart[x2] = (unsigned short)x1;
+      }
+      x += c | (c > 0) << 16;
     }
   }
   __syncthreads();
-  const int U = urank[M - 1] + (cnt[M - 1] > 0);
-  if (tid == 0) {
+  const int U = misc[1];
+  if (tid == 0 && part == 0) {
     atomicAdd(&p.stats[0], static_cast<unsigned long long>(U));
     atomicAdd(&p.stats[1], static_cast<unsigned long long>(i_hi - i_lo));
   }
-  for (int i = i_lo + tid; i < i_hi; i += kKerThreads) {
+  for (int i = i_lo + tid; i < i_hi; i += blockDim.x) {
     const int r = sl[i];
     const int pos = start[r] + atomicAdd(&fill[r], 1);
-    pairs[pos] = short(i);  // i = s * n + k
-    pair_s[pos] = static_cast<unsigned char>(i / n);
+    const int s = i / n, k = i - s * n;  // i = s * n + k
+    // K_red offset of (s, k) | k << 18 | s << 24 (offset < 100 * 2016 < 2^18)
+    pairs[pos] = uint32_t(s * ntri + k * (k - 1) / 2) | uint32_t(k) << 18 | uint32_t(s) << 24;
   }
+  __syncthreads();  // pairs built; the row buffers now overwrite the setup arrays
   MPCMMD_STAMP(p, 17);
   const float4* Dg = reinterpret_cast<const float4*>(p.bdist + size_t(b) * M * Md);
-  const int R = C.rows, q4 = Md >> 2;
-  const int g = tid >> 3, gl = tid & 7, ng = kKerThreads >> 3;  // 8 lanes per pair
-  const int ntri = n * (n - 1) / 2;
-  const int nchunk = (U + R - 1) / R;
-  // LDS-DMA (global_load_lds_dwordx4) of chunk c into buffer c & 1: the chunk
-  // image is lane-linear (rows contiguous, no padding), each lane's source
-  // row is its own address
-  auto issue = [&](int c) {
-    const int c0 = c * R, rc = min(R, U - c0);
-    float4* dst = reinterpret_cast<float4*>(Dl + size_t(c & 1) * R * Md);
-    for (int idx = tid; idx < rc * q4; idx += kKerThreads) {
-      const int u = idx / q4, cc = idx - u * q4;
-      __builtin_amdgcn_global_load_lds(Dg + size_t(ulist[c0 + u]) * q4 + cc, dst + (idx - (tid & 63)), 16, 0, 0);
-    }
+  float4* rb4 = reinterpret_cast<float4*>(smem + C.rowbuf) + size_t(w) * (Md >> 2);
+  const float* rb = reinterpret_cast<const float*>(rb4);
+  float* kbase = p.bkred + size_t(b) * kBetaSamples * ntri;
+  // this part's rows u = part + split q, q from the workgroup's counter
+  auto grab = [&]() {
+    int q = 0;
+    if (lane == 0) q = atomicAdd(&misc[0], 1);
+    return part + split * __builtin_amdgcn_readfirstlane(q);
   };
-  __syncthreads();  // pairs built
-  if (nchunk > 0) issue(0);
-  for (int c = 0; c < nchunk; ++c) {
-    // chunk c landed (each wave waits for its own DMA), every wave is done
-    // with chunk c - 1, whose buffer chunk c + 1 now reuses
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (c + 1 < nchunk) issue(c + 1);
-    if (c == 0) MPCMMD_STAMP(p, 18);
-    const int c0 = c * R, rc = min(R, U - c0);
-    const float* Db = Dl + size_t(c & 1) * R * Md;
-    const int p0 = start[ulist[c0]];
-    const int p1 = start[ulist[c0 + rc - 1]] + cnt[ulist[c0 + rc - 1]];
-    const int nf4 = Md >> 5;  // float4s per lane of the 8-lane group
-    for (int pi = p0 + g; pi < p1; pi += ng) {
-      const int i = pairs[pi];
-      const int s = pair_s[pi];
-      const int k = i - s * n;
-      const float cn = csg[s];
-      const int u = urank[sl[i]] - c0;
-      // lane gl reads float4s gl, gl + 8, ...: the group reads 128 contiguous bytes
-      const float4* drow = reinterpret_cast<const float4*>(Db + size_t(u) * Md) + gl;
-      const f2 c2 = {cn, cn};
-      f2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f};
-#pragma unroll 4
-      for (int q = 0; q < nf4; ++q) {
-        const float4 d = drow[8 * q];
-        const f2 t0 = f2{d.x, d.y} * c2, t1 = f2{d.z, d.w} * c2;
-        a0 += f2{__builtin_amdgcn_exp2f(t0.x), __builtin_amdgcn_exp2f(t0.y)};
-        a1 += f2{__builtin_amdgcn_exp2f(t1.x), __builtin_amdgcn_exp2f(t1.y)};
+  auto load = [&](float4 (&x)[NV4], int u) {
+    const float4* src = Dg + size_t(ulist[u]) * (Md >> 2) + lane;
+#pragma unroll
+    for (int t = 0; t < NV4; ++t) x[t] = src[64 * t];
+  };
+  // one distinct row u held in x: its pairs 8 at a time, row sums and then
+  // the batch's K_red entries (8 lanes per pair, kk = lane & 7 + 8 i)
+  auto do_row = [&](const float4 (&x)[NV4], int u) {
+#pragma unroll
+    for (int t = 0; t < NV4; ++t) rb4[lane + 64 * t] = x[t];
+    wave_sync();  // the row copy is in LDS before the gathers (one wave's LDS operations run in order)
+    const int pb = ustart[u], pc = ustart[u + 1] - pb;
+    for (int c0 = 0; c0 < pc; c0 += 64) {  // (rows with more than 64 pairs: chunks)
+      // lane l holds pair c0 + l and its scale; batches broadcast them by readlane
+      const int cc = min(64, pc - c0);
+      const uint32_t pl = pairs[pb + c0 + min(lane, cc - 1)];
+      const float cl = csg[pl >> 24];
+      for (int j0 = 0; j0 < cc; j0 += 8) {
+#ifndef MPCMMD_KER_NOSUM
+        float v[8];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          v[jj] = 0.0f;
+          if (j0 + jj < cc) {
+            const float cn = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cl), j0 + jj));
+            const f2 c2 = {cn, cn};
+            f2 a0, a1;
+#pragma unroll
+            for (int t = 0; t < NV4; ++t) {
+              const f2 t0 = f2{x[t].x, x[t].y} * c2, t1 = f2{x[t].z, x[t].w} * c2;
+              const f2 e0 = {__builtin_amdgcn_exp2f(t0.x), __builtin_amdgcn_exp2f(t0.y)};
+              const f2 e1 = {__builtin_amdgcn_exp2f(t1.x), __builtin_amdgcn_exp2f(t1.y)};
+              a0 = t == 0 ? e0 : a0 + e0;
+              a1 = t == 0 ? e1 : a1 + e1;
+            }
+            a0 += a1;
+            v[jj] = a0.x + a0.y;
+          }
+        }
+        const float sum = transpose_sum8(v);
+#endif
+        // lane group j = lane >> 3 takes pair j0 + j
+        const int jg = j0 + (lane >> 3);
+        const bool live = jg < cc;
+        const uint32_t pkj = __shfl(pl, jg, 64);
+        const float cj = __shfl(cl, jg, 64);
+        const int s = pkj >> 24, k = live ? int(pkj >> 18) & 63 : 0;
+#ifndef MPCMMD_KER_NOSUM
+        if ((lane & 7) == 4 && live) rowsum[s * n + k] = double(sum);
+#endif
+#ifndef MPCMMD_KER_NOGATHER
+        const short* sls = sl + s * n;
+        float* kr = kbase + (pkj & 0x3FFFFu);
+        for (int kk = lane & 7; kk < k; kk += 8) kr[kk] = __builtin_amdgcn_exp2f(rb[sls[kk]] * cj);
+#endif
       }
-      a0 += a1;
-      // K_red[s][k][kk] for kk < k: row t_k of the distance matrix is in the chunk
-      const float* dr = Db + size_t(u) * Md;
-      float* kr = p.bkred + (size_t(b) * kBetaSamples + s) * ntri + k * (k - 1) / 2;
-      for (int kk = gl; kk < k; kk += 8) kr[kk] = __builtin_amdgcn_exp2f(dr[sl[s * n + kk]] * cn);
-      float a = a0.x + a0.y;
-      a += __shfl_xor(a, 1, 8);
-      a += __shfl_xor(a, 2, 8);
-      a += __shfl_xor(a, 4, 8);
-      if (gl == 0) rowsum[i] = double(a);
     }
-    if (c == 0) MPCMMD_STAMP(p, 19);
+    wave_sync();  // the gathers read the copy before the next row overwrites it
+  };
+  float4 d[NV4];
+  int u = grab();
+  if (kPrefetch) {
+    // ping-pong: the next row's loads are issued (unconditionally, a past-the-
+    // end index clamped to the current row) before the current row is summed,
+    // so the memory-counter waits are exact and the loads overlap the exps
+    float4 dn[NV4];
+    if (u < U) load(d, u);
+    while (u < U) {
+      const int un = grab();
+      load(dn, un < U ? un : u);
+      do_row(d, u);
+      if (un >= U) break;
+      const int unn = grab();
+      load(d, unn < U ? unn : un);
+      do_row(dn, un);
+      u = unn;
+    }
+  } else {
+    for (; u < U; u = grab()) {
+      load(d, u);
+      do_row(d, u);
+    }
   }
   MPCMMD_STAMP(p, 20);
+#ifdef MPCMMD_WGT
+  __syncthreads();
+  if (tid == 0) p.wgt[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // ------------------------------------------------------------------------
@@ -1363,9 +1474,8 @@ bool mmdopt_supported(int n, int H, int O, std::string* why) {
     if (why) *why = "mmd_opt needs num_reduced <= 64";
     return false;
   }
-  const KerLds k = ker_lds(M, n, kLdsBudget);
-  if (k.rows < 1 || k.total > kLdsBudget) {
-    if (why) *why = "mmd_opt: num_reduced^2 too large for the LDS-staged kernel-sum stage";
+  if (ker_lds(M, n, ker_waves(M, n)).total > kLdsBudget) {
+    if (why) *why = "mmd_opt: num_reduced^2 too large for the kernel-sum stage";
     return false;
   }
   const EliteLds e = elite_lds(M + 1);
@@ -1455,11 +1565,34 @@ void launch_bqp(const Params& p, int tb, hipStream_t s) {
   }
 }
 
+template <int NV4>
+void launch_bkernel_v(const Params& p, int tb, int wv, int split, hipStream_t s) {
+  const KerLds k = ker_lds(p.M, p.n, wv);
+  hipLaunchKernelGGL((k_bkernel<NV4>), dim3(p.nb * split), dim3(64 * wv), k.total, s, p, tb, split);
+}
+
 void launch_bkernel(const Params& p, int tb, hipStream_t s) {
-  size_t budget = kKerHalfBudget;
-  if (ker_lds(p.M, p.n, budget).rows < kKerMinRowsHalf) budget = kLdsBudget;
-  const KerLds k = ker_lds(p.M, p.n, budget);
-  hipLaunchKernelGGL(k_bkernel, dim3(p.nb), dim3(kKerThreads), k.total, s, p, tb, int(budget));
+  const int wv = ker_waves(p.M, p.n);
+  // parts per candidate: enough workgroups to fill the chip
+  int split = 1;
+  while (split < 8 && p.nb * split < 512) split <<= 1;
+  static const int split_env = [] {
+    const char* e = std::getenv("MPCMMD_KER_SPLIT");  // experiments: parts per candidate
+    return e ? std::atoi(e) : 0;
+  }();
+  if (split_env > 0) split = split_env;
+  switch (dist_stride(p.M) >> 8) {
+#define MPCMMD_KER_CASE(V) \
+  case V:                  \
+    return launch_bkernel_v<V>(p, tb, wv, split, s);
+    MPCMMD_KER_CASE(1) MPCMMD_KER_CASE(2) MPCMMD_KER_CASE(3) MPCMMD_KER_CASE(4)
+    MPCMMD_KER_CASE(5) MPCMMD_KER_CASE(6) MPCMMD_KER_CASE(7) MPCMMD_KER_CASE(8)
+    MPCMMD_KER_CASE(9) MPCMMD_KER_CASE(10) MPCMMD_KER_CASE(11) MPCMMD_KER_CASE(12)
+    MPCMMD_KER_CASE(13) MPCMMD_KER_CASE(14) MPCMMD_KER_CASE(15)
+    default:
+      return launch_bkernel_v<16>(p, tb, wv, split, s);
+#undef MPCMMD_KER_CASE
+  }
 }
 
 void launch_belite(const Params& p, int tb, hipStream_t s) {

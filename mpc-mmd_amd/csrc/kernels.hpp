@@ -30,9 +30,10 @@ HDI_CONST int ygen_stride(int M) { return ((M + 1) + 31) & ~31; }
 // kBzCols samples
 constexpr int kBzCols = 96;
 HDI_CONST int pos_pad(int M) { return ((M + 1) + 31) & ~31; }  // whole pairs of 16-blocks
-// row stride (floats) of the mother distance matrix: whole float4s for each
-// lane of an 8-lane group (k_bkernel); pad columns hold +inf
-HDI_CONST int dist_stride(int M) { return (M + 31) & ~31; }
+// row stride (floats) of the mother distance matrix: whole 256-column blocks
+// (k_bkernel: a wave holds a row as one float4 per lane and block); pad
+// columns hold +inf
+HDI_CONST int dist_stride(int M) { return (M + 255) & ~255; }
 
 struct Params {
   // shapes / configuration.  A launch covers G configurations of B
@@ -112,6 +113,9 @@ struct Params {
   // work counters for the roofline, summed over k_bkernel workgroups:
   // [0] distinct distance rows staged, [1] (sample, reduced row) pairs summed
   unsigned long long* stats;  // [8]
+  // per-workgroup (start, end) stamps of the last k_bkernel launch, written
+  // only by builds with -DMPCMMD_WGT (scheduling experiments)
+  unsigned long long* wgt;    // [8 Bt][2]
   // outputs
   float* results;          // [G][T][kResultStride]
   int32_t* tr_proj;        // [G][T][B]

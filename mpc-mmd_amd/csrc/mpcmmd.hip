@@ -502,6 +502,7 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     p.res_beta = (float*)h->alloc("res_beta", BT * kBetaIters * 4);
     p.dbg = (unsigned long long*)h->alloc("dbg", 64 * 8);
     p.stats = (unsigned long long*)h->alloc("stats", 8 * 8);
+    p.wgt = (unsigned long long*)h->alloc("wgt", BT * 8 * 2 * 8);
     p.results = (float*)h->alloc("results", size_t(GM) * T * kResultStride * 4);
     p.tr_proj = (int32_t*)h->alloc("tr_proj", size_t(GM) * T * B * 4);
     p.tr_obs = (int32_t*)h->alloc("tr_obs", size_t(GM) * T * kEliteCost * 4);

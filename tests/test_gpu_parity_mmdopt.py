@@ -118,8 +118,15 @@ def test_beta_cem_lockstep(native, n, B, H, O, variant, check, qp_iters):
         nat.run_stage(6, tb)
         btop = nat.read("btop").reshape(B, 100, n)
         bcost = nat.read("bcost").reshape(B, 100)
+        brow = nat.read("brow", F64, (B, 100, n))
+        kred = nat.read("bkred", F32, (B, 100, n * (n - 1) // 2))
+        lo = np.tril_indices(n, -1)   # k_bkernel's K_red layout: entry (k, kk < k) at k (k - 1) / 2 + kk
+        s_lo = 11 if tb > 0 else 0    # later iterations: rows 0..10 are the carried elites
         for b in cand if qp_iters is None or tb in qp_iters else []:
-            beta, cost, _, _ = bc.reduced_qp(p, Fb[b], bsel[b].astype(np.int64), bsig[b], M, Db[b])
+            beta, cost, K_red, rowsum = bc.reduced_qp(p, Fb[b], bsel[b].astype(np.int64), bsig[b], M, Db[b])
+            # K_mixed row sums (fp32 terms, fp32 partial sums on the GPU vs fp64 in the oracle) and K_red
+            close(f"brow[{tb},{b}]", brow[b, s_lo:], rowsum[s_lo:], rtol=1e-5, atol=0)
+            close(f"kred[{tb},{b}]", kred[b, s_lo:], K_red[s_lo:, lo[0], lo[1]], rtol=1e-6, atol=1e-7)
             close(f"btop[{tb},{b}]", btop[b], beta, rtol=1e-3, atol=1e-4)
             close(f"bcost[{tb},{b}]", bcost[b], cost, rtol=1e-4, atol=1e-4)
         nat.run_stage(7, tb)
