@@ -77,9 +77,24 @@ HDI void philox_normals4(uint32_t k0, uint32_t k1, uint32_t stream, uint32_t wor
 // the squeeze u < 1 - 0.0331 x^4 first, the exact log test only when it
 // fails (Marsaglia & Tsang 2000; oracle/rng.py:_log_gamma_parts applies the
 // identical two tests in the identical order).
+// The exact test lu < 0.5 x^2 + d - d v3 + d log(v3) is first decided in
+// fp32 (v_log_f32) and re-evaluated in fp64 only when the two sides lie
+// within a bound far above the fp32 evaluation error: the same decision as
+// the fp64 test, without an fp64 log (a ~50-instruction expansion) per attempt.
+HDI bool mt_log_test(double x, double lu, double d, double v3) {
+#ifdef __HIP_DEVICE_COMPILE__
+  const float xf = float(x), df = float(d), v3f = float(v3), luf = float(lu);
+  const float q = 0.5f * xf * xf, dv = df * v3f, dl = df * (__builtin_amdgcn_logf(v3f) * 0.693147180559945309f);
+  const float rhs = ((q + df) - dv) + dl;
+  const float tol = 1e-5f * (1.0f + fabsf(luf) + q + fabsf(df) + fabsf(dv) + fabsf(dl));
+  if (luf < rhs - tol) return true;
+  if (luf > rhs + tol) return false;
+#endif
+  return lu < 0.5 * x * x + d - d * v3 + d * log(v3);
+}
 HDI bool mt_accept(double x, double u, double lu, double d, double v3) {
   if (u < 1.0 - 0.0331 * (x * x) * (x * x)) return true;
-  return lu < 0.5 * x * x + d - d * v3 + d * log(v3);
+  return mt_log_test(x, lu, d, v3);
 }
 
 // One Marsaglia-Tsang attempt from the Philox counter (elem, k, stream, 1):
@@ -108,7 +123,6 @@ HDI GammaAttempt gamma_attempt(uint32_t k0, uint32_t k1, uint32_t stream, uint32
 // candidate applies only its own (alpha-dependent) transform.  Layout
 // [stream 0..3][k][field 0..3][h][r] (r fastest: coalesced per sample row).
 constexpr int kGammaTabAttempts = 4;
-constexpr double kBoostLinMin = -600.0;  // exp(-600) ~ 1e-261: no underflow in G' U^(1/alpha)
 constexpr int kGammaTabStreams = 4;  // acc A, acc B, steer A, steer B
 HDI size_t gamma_tab_size(int S, int H) { return size_t(kGammaTabStreams) * kGammaTabAttempts * 4 * S * H; }
 
@@ -155,6 +169,27 @@ DEVI void gamma_parts_tab(MtConst mc, const double* tab, int S, int H, int r, in
   }
 }
 
+// Beta(a, b) = Ga / (Ga + Gb) from the two gammas' G' and boost log-uniforms
+// (G = G' U^(1/alpha) for alpha < 1):  1 / (1 + 2^d) with
+//   d = log2 Gb - log2 Ga = log2 gb - log2 ga + log2(e) (ub/b - ua/a).
+// The boost difference (two large, close terms for a small control) is
+// formed in fp64 as one fraction (ub a - ua b) / (a b) and rounded once (a
+// huge |d| saturates the draw at 0 or 1 through inf, as the fp64 form does); the
+// rest is fp32 (v_log_f32, v_exp_f32, v_rcp_f32).  Versus the oracle's fp64
+// evaluation (oracle/rng.py:beta_draws) the draw differs by a few ulp where it
+// is not saturated at 0 or 1 (tests/test_gpu_parity_baseline.py states the
+// tolerance); the accept / reject decisions of the gammas stay fp64 and exact.
+DEVI float beta_combine(double a, double b, double ra, double rb, double ga, double ua, double gb, double ub) {
+  if (a == 0.0 && b == 0.0) return (ua * rb > ub * ra) ? 1.0f : 0.0f;
+  const bool ka = a < 1.0, kb = b < 1.0;
+  const double fa = ka ? a : 1.0, fb = kb ? b : 1.0;
+  const double num = (kb ? ub : 0.0) * fa - (ka ? ua : 0.0) * fb;
+  const float e = float(num * __builtin_amdgcn_rcp(fa * fb));  // v_rcp_f64: fp64 range for tiny controls
+  const float d = (__builtin_amdgcn_logf(float(gb)) - __builtin_amdgcn_logf(float(ga))) +
+                  1.44269504088896340736f * e;
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(d));
+}
+
 // Beta(a, b) with a = ra*s, b = rb*s (s = |control|); s == 0 takes the
 // alpha -> 0+ limit (oracle/rng.py:beta_draws, DESIGN.md Numerics).  tab_a,
 // tab_b: the attempt-table slices of the two gamma streams.
@@ -166,30 +201,16 @@ DEVI float beta_draw_tab(double a, double b, double ra, double rb, MtConst mc_a,
   double ga, ua, gb, ub;
   gamma_parts_tab(mc_a, tab_a, S, H, r, h, k0, k1, stream_a, elem, ga, ua);
   gamma_parts_tab(mc_b, tab_b, S, H, r, h, k0, k1, stream_b, elem, gb, ub);
-  if (a == 0.0 && b == 0.0) return (ua * rb > ub * ra) ? 1.0f : 0.0f;
-  // G = G' U^(1/alpha) for alpha < 1 (boost); linear space while the boost
-  // factors cannot underflow, log space otherwise
-  const double ba = a < 1.0 ? ua / a : 0.0, bb = b < 1.0 ? ub / b : 0.0;
-  if (ba > kBoostLinMin && bb > kBoostLinMin) {
-    const double Ga = ga * (a < 1.0 ? exp(ba) : 1.0), Gb = gb * (b < 1.0 ? exp(bb) : 1.0);
-    return float(Ga / (Ga + Gb));
-  }
-  const double la = log(ga) + ba, lb = log(gb) + bb;
-  // exp(la - lm), exp(lb - lm) with lm = max(la, lb): one of them is exp(0) = 1 exactly
-  if (la > lb) {
-    const double eb = exp(lb - la);
-    return float(1.0 / (1.0 + eb));
-  }
-  const double ea = exp(la - lb);
-  return float(ea / (ea + 1.0));
+  return beta_combine(a, b, ra, rb, ga, ua, gb, ub);
 }
 
 // Table-only fast path of beta_draw_tab for the hot plane kernel: returns
 // false (and leaves `out`) when a gamma needs more than the tabulated
 // attempts (rare); the caller then defers
 // the element to the full beta_draw_tab (identical arithmetic).
-DEVI bool gamma_tab_only(MtConst mc, const double* tab, size_t plane, size_t at, double& g, double& lub) {
-  for (int k = 0; k < kGammaTabAttempts; ++k) {
+// attempts k0 .. kGammaTabAttempts - 1 of the table
+DEVI bool gamma_tab_from(MtConst mc, const double* tab, size_t plane, size_t at, int k0, double& g, double& lub) {
+  for (int k = k0; k < kGammaTabAttempts; ++k) {
     const double* t = tab + size_t(k) * 4 * plane + at;
     const double x = t[0];
     const double v = 1.0 + mc.c * x;
@@ -204,29 +225,33 @@ DEVI bool gamma_tab_only(MtConst mc, const double* tab, size_t plane, size_t at,
   }
   return false;
 }
+DEVI bool gamma_tab_only(MtConst mc, const double* tab, size_t plane, size_t at, double& g, double& lub) {
+  return gamma_tab_from(mc, tab, plane, at, 0, g, lub);
+}
+// One tabulated attempt held in registers (k_beta_planes: loaded once per
+// (row, step) and applied to several candidates' alphas).
+struct GammaAtt {
+  double x, u, lu, lw;
+};
+DEVI bool gamma_try(MtConst mc, const GammaAtt& t, double& g, double& lub) {
+  const double v = 1.0 + mc.c * t.x;
+  if (v > 0.0) {
+    const double v3 = v * v * v;
+    if (mt_accept(t.x, t.u, t.lu, mc.d, v3)) {
+      g = mc.d * v3;
+      lub = t.lw;
+      return true;
+    }
+  }
+  return false;
+}
 DEVI bool beta_draw_fast(double a, double b, double ra, double rb, MtConst mc_a, MtConst mc_b, const double* tab_a,
                          const double* tab_b, int S, int H, int r, int h, float& out) {
   const size_t plane = size_t(S) * H, at = size_t(h) * S + r;
   double ga, ua, gb, ub;
   if (!gamma_tab_only(mc_a, tab_a, plane, at, ga, ua) || !gamma_tab_only(mc_b, tab_b, plane, at, gb, ub))
     return false;
-  if (a == 0.0 && b == 0.0) {
-    out = (ua * rb > ub * ra) ? 1.0f : 0.0f;
-    return true;
-  }
-  const double ba = a < 1.0 ? ua / a : 0.0, bb = b < 1.0 ? ub / b : 0.0;
-  if (ba > kBoostLinMin && bb > kBoostLinMin) {
-    const double Ga = ga * (a < 1.0 ? exp(ba) : 1.0), Gb = gb * (b < 1.0 ? exp(bb) : 1.0);
-    out = float(Ga / (Ga + Gb));
-    return true;
-  }
-  const double la = log(ga) + ba, lb = log(gb) + bb;
-  if (la > lb) {
-    out = float(1.0 / (1.0 + exp(lb - la)));
-  } else {
-    const double ea = exp(la - lb);
-    out = float(ea / (ea + 1.0));
-  }
+  out = beta_combine(a, b, ra, rb, ga, ua, gb, ub);
   return true;
 }
 

@@ -84,6 +84,44 @@ def test_stage_lockstep(native, cost, noise):
         close("result_obs", res[23], out["obs"], atol=1e-5)
 
 
+# Beta draws (k_beta_planes / k_beta_fix): the gamma accept / reject decisions
+# are fp64 and exact, the Beta combine is fp32 on the GPU (csrc/rng.hpp:
+# beta_combine) vs fp64 in the oracle -- a few ulp where the draw is not
+# saturated at 0 or 1
+BETA_RTOL, BETA_ATOL = 1e-5, 3e-7
+
+
+def test_beta_planes(native):
+    from oracle.rng import (STREAM_GAMMA_ACC_A, STREAM_GAMMA_ACC_B, STREAM_GAMMA_STEER_A, STREAM_GAMMA_STEER_B,
+                            beta_draws, iteration_key)
+    ora, nat, xo, yo = make_pair(native, "cvar", "beta", n=N_S, O=O, H=H, B=B, T=T, acc_c=0.05, steer_c=0.01)
+    draws = oracle.Draws.random(ora.prob, np.random.default_rng(3), idx_mpc=123, seed=0, with_beta_cem=False)
+    nat.begin("cvar", 123, DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, xo, yo, 15.0, draws)
+    p = ora.prob
+    worst = 0.0
+    for t in range(2):
+        nat.run_stage(1, t)
+        nat.run_stage(2, t)
+        acc = nat.read("acc").reshape(B, 100)[:, :H]
+        steer = nat.read("steer").reshape(B, 100)[:, :H]
+        planes = nat.read("bplane", np.float32, (B, 2, H, N_S))
+        key = iteration_key(123, t, draws.seed)
+        elem = np.arange(N_S, dtype=np.uint64)[:, None] * np.uint64(H) + np.arange(H, dtype=np.uint64)[None, :]
+        elem = np.broadcast_to(elem, (B, N_S, H))
+        for k, (ctl, sa, sb) in enumerate([(acc, STREAM_GAMMA_ACC_A, STREAM_GAMMA_ACC_B),
+                                           (steer, STREAM_GAMMA_STEER_A, STREAM_GAMMA_STEER_B)]):
+            c = np.broadcast_to(np.abs(ctl)[:, None, :], (B, N_S, H))
+            ref = beta_draws((np.float32(p.beta_a) * c).astype(np.float64),
+                             (np.float32(p.beta_b) * c).astype(np.float64), key, sa, sb, elem)
+            got = planes[:, k].transpose(0, 2, 1)
+            err = np.abs(got.astype(np.float64) - ref)
+            lim = BETA_ATOL + BETA_RTOL * np.abs(ref)
+            assert np.all(err <= lim), f"beta plane {k} t={t}: {int((err > lim).sum())} outside, worst {err.max():.3g}"
+            worst = max(worst, float((err / np.maximum(np.abs(ref), 1e-30)).max()))
+        nat.run_stage(3, t)
+    print(f"Beta draws: worst relative difference {worst:.3g}")
+
+
 def run_iteration_lockstep(native, cost, noise, Tf=20, n=N_S, B=B, H=H, O=O, seed=7, idx=5):
     """20 full GPU iterations (noise, front, risk, select).  Before each, the
     oracle is synchronised to the GPU's carry and runs the same iteration on
