@@ -155,7 +155,8 @@ __global__ __launch_bounds__(256) void k_gamma_tab(Params p, int t) {
   o[0] = g.x;
   o[plane] = g.u;
   o[2 * size_t(plane)] = g.lu;
-  o[3 * size_t(plane)] = g.lw;
+  const bool squeeze = g.u < 1.0 - 0.0331 * (g.x * g.x) * (g.x * g.x);  // alpha-independent (rng.hpp)
+  o[3 * size_t(plane)] = squeeze ? g.lw : -g.lw;
 }
 
 // Beta draws of every (candidate, row, step) of the baseline rollouts:

@@ -116,7 +116,10 @@ HDI GammaAttempt gamma_attempt(uint32_t k0, uint32_t k1, uint32_t stream, uint32
 }
 
 // Attempt table of one outer iteration: the Philox-derived (x, u, log u,
-// log w) of attempts 0..kGammaTabAttempts-1 for every (stream, row r, step h).
+// +-log w) of attempts 0..kGammaTabAttempts-1 for every (stream, row r, step h).
+// The squeeze test u < 1 - 0.0331 x^4 does not depend on alpha, so it is
+// evaluated once when the table is built and stored as the sign of the
+// log w field (log w < 0 always): negative = the squeeze accepts.
 // The uniforms of the Beta noise depend only on (key, stream, r, h) -- the
 // same realisation for every candidate (cem_helper.py:110, Q2) -- so they
 // are drawn once per iteration instead of once per candidate; each
@@ -136,6 +139,22 @@ HDI MtConst mt_const(double alpha) {
   const double d = a1 - 1.0 / 3.0;
   return MtConst{d, 1.0 / sqrt(9.0 * d)};
 }
+// One tabulated attempt t (fields x, u, log u, +-log w at stride plane):
+// Marsaglia-Tsang acceptance with the stored squeeze decision
+DEVI bool tab_attempt(MtConst mc, const double* t, size_t plane, double& g, double& lub) {
+  const double x = t[0];
+  const double v = 1.0 + mc.c * x;
+  if (v > 0.0) {
+    const double v3 = v * v * v;
+    const double lw = t[3 * plane];
+    if (lw < 0.0 || mt_log_test(x, t[2 * plane], mc.d, v3)) {
+      g = mc.d * v3;
+      lub = -fabs(lw);
+      return true;
+    }
+  }
+  return false;
+}
 DEVI void gamma_parts_tab(MtConst mc, const double* tab, int S, int H, int r, int h, uint32_t k0, uint32_t k1,
                           uint32_t stream, uint32_t elem, double& g, double& lub) {
   const double d = mc.d, c = mc.c;
@@ -143,17 +162,7 @@ DEVI void gamma_parts_tab(MtConst mc, const double* tab, int S, int H, int r, in
   g = d;
   lub = 0.0;
   for (int k = 0; k < kGammaTabAttempts; ++k) {
-    const double* t = tab + size_t(k) * 4 * plane + at;
-    const double x = t[0];
-    const double v = 1.0 + c * x;
-    if (v > 0.0) {
-      const double v3 = v * v * v;
-      if (mt_accept(x, t[plane], t[2 * plane], d, v3)) {
-        g = d * v3;
-        lub = t[3 * plane];
-        return;
-      }
-    }
+    if (tab_attempt(mc, tab + size_t(k) * 4 * plane + at, plane, g, lub)) return;
   }
   for (int k = kGammaTabAttempts; k < kGammaMaxAttempts; ++k) {
     const GammaAttempt ga = gamma_attempt(k0, k1, stream, elem, k);
@@ -210,19 +219,8 @@ DEVI float beta_draw_tab(double a, double b, double ra, double rb, MtConst mc_a,
 // the element to the full beta_draw_tab (identical arithmetic).
 // attempts k0 .. kGammaTabAttempts - 1 of the table
 DEVI bool gamma_tab_from(MtConst mc, const double* tab, size_t plane, size_t at, int k0, double& g, double& lub) {
-  for (int k = k0; k < kGammaTabAttempts; ++k) {
-    const double* t = tab + size_t(k) * 4 * plane + at;
-    const double x = t[0];
-    const double v = 1.0 + mc.c * x;
-    if (v > 0.0) {
-      const double v3 = v * v * v;
-      if (mt_accept(x, t[plane], t[2 * plane], mc.d, v3)) {
-        g = mc.d * v3;
-        lub = t[3 * plane];
-        return true;
-      }
-    }
-  }
+  for (int k = k0; k < kGammaTabAttempts; ++k)
+    if (tab_attempt(mc, tab + size_t(k) * 4 * plane + at, plane, g, lub)) return true;
   return false;
 }
 DEVI bool gamma_tab_only(MtConst mc, const double* tab, size_t plane, size_t at, double& g, double& lub) {
