@@ -323,24 +323,119 @@ DEVI void emit_top(const uint32_t* key, uint32_t T, bool exact, int n, int32_t* 
   wave_sync();
 }
 
-// Top-n selection for the samples s = first, first + stride, ... < last of
-// one wave, NB at a time: keys of NB samples are loaded together and their
-// threshold searches interleave.  row(s) -> values, out(s) -> int32[n].
-template <int NQ, class Row, class Out>
-DEVI void select_batch(Row row, Out out, int first, int last, int stride, int M, int n, int* scratch) {
-  constexpr int NB = NQ <= 8 ? 4 : (NQ <= 16 ? 2 : 1);
-  for (int s0 = first; s0 < last; s0 += NB * stride) {
-    uint32_t key[NB][NQ];
-    const int nb = min(NB, (last - s0 + stride - 1) / stride);
+// Window top-n.  Given a threshold T with n <= c = #{keys >= T}, the keys
+// >= T are compacted into LDS as 64-bit words (key << 32 | j), whose unsigned
+// order is the jnp.argsort order (ascending |v|, ties by index); if c <= 64 R
+// each lane ranks R of them exactly (one broadcast LDS read and one 64-bit
+// compare per candidate, no scalar-unit chains) and the top n go to out[] in
+// argsort order (out[n - 1 - rank], rank 0 = largest).  Returns false (and
+// writes nothing) when c > 64 R.
+template <int NQ, int R>
+DEVI bool emit_window(const uint32_t* key, uint32_t T, int n, int32_t* out, unsigned long long* cand) {
+  constexpr int cap = 64 * R;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int c = 0;
 #pragma unroll
-    for (int u = 0; u < NB; ++u)  // unconditional (clamped) loads: one memory latency
-      load_keys<NQ>(row(min(s0 + u * stride, last - 1)), M, key[u]);
-    uint32_t T[NB];
-    bool exact[NB];
-    find_thresholds<NQ, NB>(key, nb, n, T, exact);
+  for (int q = 0; q < NQ; ++q) {
+    const bool sel = key[q] >= T;
+    const unsigned long long m = __ballot(sel);
+    const int pos = c + __popcll(m & below);
+    // unconditional store: overflow and unselected lanes write the dump slot
+    cand[sel && pos < cap ? pos : cap + 3] = (static_cast<unsigned long long>(key[q]) << 32) | uint32_t(lane + 64 * q);
+    c += __popcll(m);
+  }
+  if (c > cap) return false;
+  if (lane < 2) cand[c + lane] = 0ull;  // pad the pair read past c (ranks nothing: real keys have bit 31 set)
+  wave_sync();
+  unsigned long long mine[R];
+  int rank[R];
 #pragma unroll
-    for (int u = 0; u < NB; ++u)
-      if (u < nb) emit_top<NQ>(key[u], T[u], exact[u], n, out(s0 + u * stride), scratch);
+  for (int r = 0; r < R; ++r) {
+    mine[r] = cand[lane + 64 * r];  // slots >= c are stale; never emitted
+    rank[r] = 0;
+  }
+  const ulonglong2* c2 = reinterpret_cast<const ulonglong2*>(cand);
+  for (int e = 0; e < c; e += 2) {
+    const ulonglong2 v = c2[e >> 1];  // wave-uniform address: LDS broadcast
+#pragma unroll
+    for (int r = 0; r < R; ++r) rank[r] += int(v.x > mine[r]) + int(v.y > mine[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (lane + 64 * r < c && rank[r] < n) out[n - 1 - rank[r]] = int32_t(uint32_t(mine[r]));
+  wave_sync();
+  return true;
+}
+
+// wave minimum (VALU: quad / row butterflies, then the row broadcasts into
+// lane 63; rows a broadcast does not write keep the identity)
+template <int CTRL, int ROWS = 0xF>
+DEVI uint32_t dpp_umin_src(uint32_t v) {
+  return uint32_t(__builtin_amdgcn_update_dpp(-1, int(v), CTRL, ROWS, 0xF, false));
+}
+DEVI uint32_t wave_min_u32(uint32_t v) {
+  v = min(v, dpp_umin_src<0xB1>(v));
+  v = min(v, dpp_umin_src<0x4E>(v));
+  v = min(v, dpp_umin_src<0x124>(v));
+  v = min(v, dpp_umin_src<0x128>(v));
+  v = min(v, dpp_umin_src<0x142, 0xA>(v));
+  v = min(v, dpp_umin_src<0x143, 0xC>(v));
+  return uint32_t(__builtin_amdgcn_readlane(int(v), 63));
+}
+
+// A threshold T0 with #{keys >= T0} >= n and few keys above it: the n-th
+// largest of the G group maxima (groups of 64 / G lanes; each of the n groups
+// whose maximum is >= T0 holds a key >= T0).  For the top 22 of 484 keys in
+// 32 lane pairs about 37 keys lie above it.  Ranks by broadcast LDS reads,
+// the pick by a wave minimum; lm: G words of the wave's LDS.
+template <int NQ, int G>
+DEVI uint32_t group_max_threshold(const uint32_t* key, int n, uint32_t* lm) {
+  const int lane = threadIdx.x & 63;
+  uint32_t m = key[0];
+#pragma unroll
+  for (int q = 1; q < NQ; ++q) m = max(m, key[q]);
+  if constexpr (G == 32) m = max(m, uint32_t(__builtin_amdgcn_update_dpp(0, int(m), 0xB1, 0xF, 0xF, false)));
+  if (lane % (64 / G) == 0) lm[lane / (64 / G)] = m;
+  wave_sync();
+  int gt = 0;
+  const uint4* l4 = reinterpret_cast<const uint4*>(lm);
+#pragma unroll
+  for (int e = 0; e < G / 4; ++e) {
+    const uint4 v = l4[e];  // broadcast
+    gt += int(v.x > m) + int(v.y > m) + int(v.z > m) + int(v.w > m);
+  }
+  const uint32_t t = wave_min_u32(gt < n ? m : 0xFFFFFFFFu);
+  wave_sync();
+  return t;
+}
+
+// Top-n of the samples s = first, first + stride, ... < last, one wave, the
+// next sample's keys in flight while one is ranked.  With M <= 64 R every key
+// is a candidate; otherwise the window threshold comes from the group maxima
+// (G = 32 lane pairs for n <= 24, 64 lanes for n <= 48).  Larger n, and ties
+// so massive that the window overflows, take the exact bit bisection
+// (find_thresholds) and the ballot emission (emit_top).
+template <int NQ, int R, int G, class Row, class Out>
+DEVI void select_walk(Row row, Out out, int first, int last, int stride, int M, int n, unsigned long long* cand,
+                      uint32_t* lm, int* scratch) {
+  uint32_t key[NQ], nxt[NQ];
+  load_keys<NQ>(row(first), M, key);
+  for (int s = first; s < last; s += stride) {
+    load_keys<NQ>(row(min(s + stride, last - 1)), M, nxt);  // next sample's keys in flight
+    bool done = false;
+    if (M <= 64 * R)
+      done = emit_window<NQ, R>(key, 0x80000000u, n, out(s), cand);  // real keys have bit 31 set
+    else if (G > 0 && n <= G * 3 / 4)
+      done = emit_window<NQ, R>(key, group_max_threshold<NQ, (G > 0 ? G : 64)>(key, n, lm), n, out(s), cand);
+    if (!done) {
+      uint32_t Tn[1];
+      bool ex[1];
+      find_thresholds<NQ, 1>(&key, 1, n, Tn, ex);
+      emit_top<NQ>(key, Tn[0], ex[0], n, out(s), scratch);
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) key[q] = nxt[q];
   }
 }
 
@@ -485,16 +580,17 @@ __global__ __launch_bounds__(64 * kSampleWaves) void k_bsample(Params p, int tb)
 
 // ------------------------------------------------------------------------
 // k_bselect: top-n |beta| rows (compute_beta.py:117-118) and sigma of the
-// 100 samples.  Latency-bound per wave, so it runs as many single-wave
-// workgroups: wave (b, g) handles samples g, g+25, g+50, g+75.
-constexpr int kSelGroups = 25;
-
-// NQ = keys per lane (M <= 64 NQ): one instantiation per size, so each has
-// its own register allocation
-template <int NQ>
+// 100 samples.  Single-wave workgroups, W = gridDim.y waves per candidate;
+// wave (b, g) walks samples g, g + W, g + 2W, ... (select_walk).
+// NQ = keys per lane (M <= 64 NQ), R = window capacity / 64, G = groups for
+// the window threshold (0: bisection): one instantiation per size, so each
+// has its own register allocation
+template <int NQ, int R, int G>
 __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
+  __shared__ __attribute__((aligned(16))) unsigned long long cand[64 * R + 4];
+  __shared__ __attribute__((aligned(16))) uint32_t lm[64];
   __shared__ int scratch[128];
-  const int b = p.b0 + blockIdx.x, g = blockIdx.y, M = p.M, M1 = M + 1, n = p.n;
+  const int b = p.b0 + blockIdx.x, g = blockIdx.y, W = gridDim.y, M = p.M, M1 = M + 1, n = p.n;
   int32_t* sel = p.bsel + size_t(b) * kBetaSamples * n;
   float* sig = p.bsig + size_t(b) * kBetaSamples;
   const float* E = p.belite + (size_t(tb & 1) * p.Bt + b) * kBetaElite * M1;
@@ -511,9 +607,9 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
   // samples 0..10 of iteration tb >= 1 are the previous elites, whose rows
   // and sigma k_belite carried over
   const int s_lo = first_sample(tb);
-  select_batch<NQ>(row, [&](int s) { return sel + s * n; }, s_lo + g, kBetaSamples, kSelGroups, M, n, scratch);
-  const int s = s_lo + g + int(threadIdx.x) * kSelGroups;
-  if (threadIdx.x < 4 && s < kBetaSamples) {
+  if (s_lo + g >= kBetaSamples) return;
+  select_walk<NQ, R, G>(row, [&](int s) { return sel + s * n; }, s_lo + g, kBetaSamples, W, M, n, cand, lm, scratch);
+  for (int s = s_lo + g + int(threadIdx.x) * W; threadIdx.x < 16 && s < kBetaSamples; s += 16 * W) {
     const float v = row(s)(M);
     sig[s] = tb == 0 ? fmaxf(v, 0.01f) : v;  // later rows are clipped when written
   }
@@ -1501,9 +1597,25 @@ void launch_bsample(const Params& p, int tb, hipStream_t s) {
   hipLaunchKernelGGL(k_bsample, dim3(p.nb), dim3(64 * kSampleWaves), 0, s, p, tb);
 }
 
+// waves per candidate: ~8 single-wave workgroups per SIMD over the launch
+int sel_waves(int nb) {
+  static const int env = [] {
+    const char* e = std::getenv("MPCMMD_SEL_WAVES");  // experiments: waves per candidate
+    return e ? std::atoi(e) : 0;
+  }();
+  if (env > 0) return env;
+  return std::max(4, std::min(25, 8192 / std::max(1, nb)));
+}
+
 template <int NQ>
 void launch_bselect_q(const Params& p, int tb, hipStream_t s) {
-  hipLaunchKernelGGL(k_bselect<NQ>, dim3(p.nb, kSelGroups), dim3(64), 0, s, p, tb);
+  const dim3 grid(p.nb, sel_waves(p.nb));
+  if (p.n <= 24)
+    hipLaunchKernelGGL((k_bselect<NQ, 1, 32>), grid, dim3(64), 0, s, p, tb);
+  else if (p.n <= 48)
+    hipLaunchKernelGGL((k_bselect<NQ, 2, 64>), grid, dim3(64), 0, s, p, tb);
+  else
+    hipLaunchKernelGGL((k_bselect<NQ, 2, 0>), grid, dim3(64), 0, s, p, tb);
 }
 
 void launch_bselect(const Params& p, int tb, hipStream_t s) {
@@ -1514,24 +1626,17 @@ void launch_bselect(const Params& p, int tb, hipStream_t s) {
     return launch_bselect_q<q>(p, tb, s);
     MPCMMD_SEL_CASE(1)
     MPCMMD_SEL_CASE(2)
-    MPCMMD_SEL_CASE(3)
     MPCMMD_SEL_CASE(4)
-    MPCMMD_SEL_CASE(5)
-    MPCMMD_SEL_CASE(6)
-    MPCMMD_SEL_CASE(7)
     MPCMMD_SEL_CASE(8)
-    MPCMMD_SEL_CASE(9)
-    MPCMMD_SEL_CASE(10)
-    MPCMMD_SEL_CASE(11)
-    MPCMMD_SEL_CASE(12)
-    MPCMMD_SEL_CASE(13)
-    MPCMMD_SEL_CASE(14)
-    MPCMMD_SEL_CASE(15)
     MPCMMD_SEL_CASE(16)
 #undef MPCMMD_SEL_CASE
     default:
       break;
   }
+  if (nq <= 4) return launch_bselect_q<4>(p, tb, s);
+  if (nq <= 8) return launch_bselect_q<8>(p, tb, s);
+  if (nq <= 12) return launch_bselect_q<12>(p, tb, s);
+  if (nq <= 16) return launch_bselect_q<16>(p, tb, s);
   if (nq <= 24) return launch_bselect_q<24>(p, tb, s);
   if (nq <= 32) return launch_bselect_q<32>(p, tb, s);
   if (nq <= 40) return launch_bselect_q<40>(p, tb, s);
