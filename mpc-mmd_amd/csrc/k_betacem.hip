@@ -646,8 +646,10 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
 #endif
 constexpr int kKerWavesMax = MPCMMD_KER_WAVES;
 
+constexpr int kLptBins = 128;  // pair counts per distinct row (<= 100 samples)
+
 struct KerLds {
-  size_t sel, csg, pairs, ulist, ustart, misc, rowbuf, total;
+  size_t sel, csg, pairs, ulist, ustart, order, bins, misc, rowbuf, total;
 };
 
 // persistent: sel (short), csg, pairs (K_red offset | k << 18 | s << 24), the distinct rows
@@ -666,6 +668,8 @@ HDI KerLds ker_lds(int M, int n, int waves) {
   L.pairs = take(size_t(kBetaSamples) * n * 4);
   L.ulist = take(size_t(M) * 2);
   L.ustart = take(size_t(M + 1) * 2);
+  L.order = take(size_t(M) * 2);
+  L.bins = take(kLptBins * 4);
   L.misc = take(32 * 4);  // [0] next row, [1] distinct rows, [16..31] scan wave totals
   const size_t rb = size_t(waves) * dist_stride(M) * 4, setup = size_t(M) * 10;
   L.rowbuf = take(rb > setup ? rb : setup);
@@ -724,7 +728,7 @@ DEVI float transpose_sum8(const float (&v)[8]) {
 }
 
 template <int NV4>
-__global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb, int split) {
+__global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb, int split, int lpt) {
   constexpr bool kPrefetch = NV4 <= 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int waves = blockDim.x >> 6;
@@ -738,6 +742,8 @@ __global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb,
   uint32_t* pairs = reinterpret_cast<uint32_t*>(smem + C.pairs);
   unsigned short* ulist = reinterpret_cast<unsigned short*>(smem + C.ulist);
   unsigned short* ustart = reinterpret_cast<unsigned short*>(smem + C.ustart);
+  unsigned short* order = reinterpret_cast<unsigned short*>(smem + C.order);
+  int* bins = reinterpret_cast<int*>(smem + C.bins);
   int* misc = reinterpret_cast<int*>(smem + C.misc);  // [0] next row, [1] distinct rows
   int* cnt = reinterpret_cast<int*>(smem + C.rowbuf);  // setup only
   int* fill = cnt + M;
@@ -759,6 +765,7 @@ __global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb,
     fill[r] = 0;
   }
   if (tid == 0) misc[0] = 0;
+  for (int c = tid; c < kLptBins; c += blockDim.x) bins[c] = 0;
   __syncthreads();
   for (int i = i_lo + tid; i < i_hi; i += blockDim.x) atomicAdd(&cnt[sl[i]], 1);
   __syncthreads();
@@ -809,17 +816,44 @@ __global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb,
     // K_red offset of (s, k) | k << 18 | s << 24 (offset < 100 * 2016 < 2^18)
     pairs[pos] = uint32_t(s * ntri + k * (k - 1) / 2) | uint32_t(k) << 18 | uint32_t(s) << 24;
   }
+  // grab order: heaviest rows (most pairs) first, so no wave starts a long row
+  // while the others run dry (bucket sort by pair count; the order within a
+  // bucket is arbitrary -- every row's outputs are independent of it -- so
+  // only for a candidate in one workgroup: parts of a split candidate must
+  // agree on the order)
+  if (lpt && split == 1) {
+    for (int u = tid; u < U; u += blockDim.x) atomicAdd(&bins[kLptBins - 1 - min(ustart[u + 1] - ustart[u], kLptBins - 1)], 1);
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of the 128 bins, two per lane
+      const int a = bins[2 * tid], c = bins[2 * tid + 1];
+      int x = a + c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (tid >= o) x += y;
+      }
+      bins[2 * tid] = x - a - c;
+      bins[2 * tid + 1] = x - c;
+    }
+    __syncthreads();
+    for (int u = tid; u < U; u += blockDim.x)
+      order[atomicAdd(&bins[kLptBins - 1 - min(ustart[u + 1] - ustart[u], kLptBins - 1)], 1)] = (unsigned short)u;
+  } else {
+    for (int u = tid; u < U; u += blockDim.x) order[u] = (unsigned short)u;
+  }
   __syncthreads();  // pairs built; the row buffers now overwrite the setup arrays
   MPCMMD_STAMP(p, 17);
   const float4* Dg = reinterpret_cast<const float4*>(p.bdist + size_t(b) * M * Md);
   float4* rb4 = reinterpret_cast<float4*>(smem + C.rowbuf) + size_t(w) * (Md >> 2);
   const float* rb = reinterpret_cast<const float*>(rb4);
   float* kbase = p.bkred + size_t(b) * kBetaSamples * ntri;
-  // this part's rows u = part + split q, q from the workgroup's counter
+  // this part's rows order[part + split q], q from the workgroup's counter
+  // (U: past the end)
   auto grab = [&]() {
     int q = 0;
     if (lane == 0) q = atomicAdd(&misc[0], 1);
-    return part + split * __builtin_amdgcn_readfirstlane(q);
+    const int i = part + split * __builtin_amdgcn_readfirstlane(q);
+    return i < U ? int(order[i]) : U;
   };
   auto load = [&](float4 (&x)[NV4], int u) {
     const float4* src = Dg + size_t(ulist[u]) * (Md >> 2) + lane;
@@ -1673,7 +1707,11 @@ void launch_bqp(const Params& p, int tb, hipStream_t s) {
 template <int NV4>
 void launch_bkernel_v(const Params& p, int tb, int wv, int split, hipStream_t s) {
   const KerLds k = ker_lds(p.M, p.n, wv);
-  hipLaunchKernelGGL((k_bkernel<NV4>), dim3(p.nb * split), dim3(64 * wv), k.total, s, p, tb, split);
+  static const int lpt = [] {
+    const char* e = std::getenv("MPCMMD_KER_NOLPT");  // experiments: row-index grab order
+    return e && std::atoi(e) > 0 ? 0 : 1;
+  }();
+  hipLaunchKernelGGL((k_bkernel<NV4>), dim3(p.nb * split), dim3(64 * wv), k.total, s, p, tb, split, lpt);
 }
 
 void launch_bkernel(const Params& p, int tb, hipStream_t s) {

@@ -1,25 +1,19 @@
 #!/usr/bin/env python3
-"""Per-kernel resource usage (VGPR/AGPR/occupancy/spills/LDS) of one HIP
-source compiled for gfx950:  python tools/kres.py mpc-mmd_amd/csrc/k_betacem.hip"""
+"""Per-kernel resources (VGPR / AGPR / SGPR / spills / LDS / occupancy) from a
+gfx950 assembly file:  python tools/kres.py /tmp/kb.s [name-filter]"""
 import re
-import subprocess
 import sys
 
-cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off", "-c",
-       sys.argv[1], "-o", "/tmp/kres.o", "-Rpass-analysis=kernel-resource-usage"]
-out = subprocess.run(cmd, capture_output=True, text=True).stderr
-rows, cur = [], None
-for line in out.splitlines():
-    m = re.search(r"Function Name: (\S+)", line)
-    if m:
-        cur = {"name": m.group(1)}
-        rows.append(cur)
+text = open(sys.argv[1]).read()
+flt = sys.argv[2] if len(sys.argv) > 2 else ""
+for m in re.finditer(r"\.amdhsa_kernel (\S+)\n(.*?)\.end_amdhsa_kernel", text, re.S):
+    name, body = m.group(1), m.group(2)
+    if flt not in name:
         continue
-    m = re.search(r"remark:\s+([A-Za-z ]+?)(?: \[[^]]*\])?: (\d+)", line)
-    if m and cur is not None:
-        cur[m.group(1).strip()] = m.group(2)
-for r in rows:
-    n = re.sub(r"^_ZN6mpcmmd12_GLOBAL__N_1\d+", "", r["name"])
-    g = lambda k: r.get(k, "?")
-    print(f"{n[:40]:40s} vgpr {g('VGPRs'):>4} agpr {g('AGPRs'):>4} occ {g('Occupancy'):>2} "
-          f"sspill {g('SGPRs Spill'):>5} vspill {g('VGPRs Spill'):>4} lds {g('LDS Size')}")
+    g = lambda k: (re.search(r"\.amdhsa_" + k + r" (\d+)", body) or [0, "?"])[1]
+    short = re.sub(r"^_ZN6mpcmmd12_GLOBAL__N_1\d+", "", name)[:60]
+    # the comment block emitted after the kernel body carries the occupancy
+    cm = re.search(re.escape(name) + r".*?; Occupancy: (\d+)", text, re.S)
+    sp = re.search(re.escape(name) + r".*?; ScratchSize: (\d+)", text, re.S)
+    print(f"{short:60s} vgpr {g('next_free_vgpr'):>4s} agpr_off {g('accum_offset'):>4s} sgpr {g('next_free_sgpr'):>4s} "
+          f"lds {g('group_segment_fixed_size'):>6s} scratch {sp.group(1) if sp else '?':>5s} occ {cm.group(1) if cm else '?'}")
