@@ -500,47 +500,45 @@ DEVI void load_block(SampleBlock& q, const double* G, const double* gm, const do
     for (int k = 0; k < 4; ++k) q.z[t][k] = z[size_t(p0 + 4 * k + h) * kBzCols + s0 + 16 * t + r];
 }
 
-// one block: Y = m + T Z + U S for the wave's tiles, then S += W^T Z
-DEVI void sample_block(const SampleBlock& cur, d4* S, float* Y, int p0, int M, int ys, int r, int h) {
-  // X = W_c U_c^T: register i holds w_{h+4i} . u_r = T[row r][col h + 4i]
-  d4 X = d4{0.0, 0.0, 0.0, 0.0};
+// One block's MFMAs for the wave's tiles, all accumulating in place:
+//   Y  = m + U S          (3 per tile, C operand starts at the means)
+//   S += W^T Z            (4 per tile; after U S has read S)
+//   Y += T Z              (4 per tile; T from X = W U^T, built meanwhile)
+// Tiles are interleaved, so every accumulator chain has 6 MFMAs between
+// dependent steps.  No VALU work on the accumulators: the pipe never waits
+// for a vector add between blocks.
+DEVI void block_mfma(const SampleBlock& cur, d4* S, d4* Y, int r, int h) {
+  d4 X = d4{0.0, 0.0, 0.0, 0.0};  // X = W_c U_c^T: register i holds w_{h+4i} . u_r = T[row r][col h + 4i]
 #pragma unroll
   for (int i = 0; i < 3; ++i) X = mfma64(cur.wX[i], cur.uX[i], X);
+  const d4 m = d4{cur.m[0], cur.m[1], cur.m[2], cur.m[3]};
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int t = 0; t < kTilesPerWave; ++t) Y[t] = mfma64(cur.uX[k], S[t][k], k == 0 ? m : Y[t]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int t = 0; t < kTilesPerWave; ++t) S[t] = mfma64(cur.wA[k], cur.z[t][k], S[t]);
   double T[4];  // A operand of T Z, k-step i: T[r][4i + h]
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int k = h + 4 * i;
     T[i] = k < r ? X[i] : (k == r ? cur.L : 0.0);
   }
-  // independent chains, tiles interleaved: Y = m + T Z (acc a) + U S (acc b),
-  // P = W^T Z (two partial accumulators), S += P after U S has read S
-  d4 Ya[kTilesPerWave], Yb[kTilesPerWave], P0[kTilesPerWave], P1[kTilesPerWave];
-#pragma unroll
-  for (int t = 0; t < kTilesPerWave; ++t) {
-    Ya[t] = d4{cur.m[0], cur.m[1], cur.m[2], cur.m[3]};
-    Yb[t] = d4{0.0, 0.0, 0.0, 0.0};
-    P0[t] = d4{0.0, 0.0, 0.0, 0.0};
-    P1[t] = d4{0.0, 0.0, 0.0, 0.0};
-  }
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
-    for (int t = 0; t < kTilesPerWave; ++t) {
-      if (k < 3) Yb[t] = mfma64(cur.uX[k], S[t][k], Yb[t]);
-      if (k & 1) P1[t] = mfma64(cur.wA[k], cur.z[t][k], P1[t]);
-      else P0[t] = mfma64(cur.wA[k], cur.z[t][k], P0[t]);
-    }
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-#pragma unroll
-    for (int t = 0; t < kTilesPerWave; ++t) Ya[t] = mfma64(T[k], cur.z[t][k], Ya[t]);
+    for (int t = 0; t < kTilesPerWave; ++t) Y[t] = mfma64(T[k], cur.z[t][k], Y[t]);
+}
+
+// the finished block's samples to fp32 (the sigma coordinate M clipped)
+DEVI void block_store(const d4* Yv, float* Y, int p0, int M, int ys, int h) {
 #pragma unroll
   for (int t = 0; t < kTilesPerWave; ++t) {
-    S[t] = S[t] + (P0[t] + P1[t]);
-    const d4 Yv = Ya[t] + Yb[t];
     float* yrow = Y + size_t(16 * t) * ys + p0 + h;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) yrow[4 * i] = p0 + h + 4 * i == M ? fmaxf(float(Yv[i]), 0.01f) : float(Yv[i]);
+    for (int i = 0; i < 4; ++i) yrow[4 * i] = p0 + h + 4 * i == M ? fmaxf(float(Yv[t][i]), 0.01f) : float(Yv[t][i]);
   }
 }
 
@@ -555,26 +553,32 @@ __global__ __launch_bounds__(64 * kSampleWaves) void k_bsample(Params p, int tb)
   const double* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
   const int ys = ygen_stride(M);
   float* Y = p.ygen + (size_t(b) * kBzCols + s0 + r) * ys;
-  d4 S[kTilesPerWave];
+  d4 S[kTilesPerWave], Ya[kTilesPerWave], Yb[kTilesPerWave];
 #pragma unroll
   for (int t = 0; t < kTilesPerWave; ++t) S[t] = d4{0.0, 0.0, 0.0, 0.0};
   const int nblk = Pp >> 4;
-  // blocks in pairs, operands ping-ponged: the next block's loads are in
-  // flight while this block's MFMAs run (the last prefetch re-reads a block)
-  // (nblk is even; sched barriers keep the prefetch ahead of the MFMAs)
+  // blocks in pairs, operands and outputs ping-ponged: the next block's loads
+  // are in flight and its MFMAs issued while the previous block's samples
+  // are converted and stored (the last prefetch re-reads a block; nblk is
+  // even; sched barriers keep that order)
   SampleBlock qa, qb;
   load_block(qa, G, gm, z, 0, s0, r, h);
   for (int c = 0; c < nblk; c += 2) {
     const int p0 = c << 4;
     load_block(qb, G, gm, z, p0 + 16, s0, r, h);
     __builtin_amdgcn_sched_barrier(0);
-    sample_block(qa, S, Y, p0, M, ys, r, h);
+    block_mfma(qa, S, Ya, r, h);
+    __builtin_amdgcn_sched_barrier(0);
+    if (c > 0) block_store(Yb, Y, p0 - 16, M, ys, h);
     __builtin_amdgcn_sched_barrier(0);
     load_block(qa, G, gm, z, min(p0 + 32, Pp - 16), s0, r, h);
     __builtin_amdgcn_sched_barrier(0);
-    sample_block(qb, S, Y, p0 + 16, M, ys, r, h);
+    block_mfma(qb, S, Yb, r, h);
+    __builtin_amdgcn_sched_barrier(0);
+    block_store(Ya, Y, p0, M, ys, h);
     __builtin_amdgcn_sched_barrier(0);
   }
+  block_store(Yb, Y, Pp - 16, M, ys, h);
   MPCMMD_STAMP(p, 1);
 }
 
@@ -991,7 +995,7 @@ DEVI void bqp_quad(const Params& p, int tb) {
   const double delta = cdiag - 1.0;  // C_ii - K_ii (K_ii = exp(0) = 1)
   // own rows: A[t][k] = C[4t+q][k], k <= 4t+3 (k > row: 0)
   double A[T4][NP];
-  double g[T4], a1[T4], a2[T4], rin[T4];
+  double a1[T4], a2[T4], rin[T4];
   // every load unconditional (clamped address, value masked afterwards) so
   // they are all in flight together: one memory latency, not one per entry
   float kv[T4][NP];
@@ -1011,42 +1015,43 @@ DEVI void bqp_quad(const Params& p, int tb) {
 #pragma unroll
   for (int t = 0; t < T4; ++t) {
     const int i = 4 * t + q;
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      if (k > 4 * t + 3) continue;
-      double v = (k < i && i < n) ? double(kv[t][k]) : 0.0;
-      if (k == i) v = i < n ? cdiag : 1.0;
-      A[t][k] = v;
-    }
-    g[t] = i < n ? bv[t] * inv_m : 0.0;
-    a1[t] = g[t];
+    a1[t] = i < n ? bv[t] * inv_m : 0.0;  // g
     a2[t] = i < n ? 1.0 : 0.0;
     rin[t] = 0.0;
   }
-  // Cholesky, column j
+  // Cholesky, left-looking by columns: column k of C (still fp32 in kv)
+  // minus sum_{j<k} L_ij L_kj, in the order j = 0, 1, ... (the right-looking
+  // update order, so the same roundings), then scaled.  The fp32 input of
+  // columns > k and the fp64 factor of columns < k are live together, never
+  // both in full, which keeps the kernel at two waves per SIMD.
 #pragma unroll
-  for (int j = 0; j < NP; ++j) {
-    const int tj = j >> 2, qj = j & 3;
-    const double sv = A[tj][j];
+  for (int k = 0; k < NP; ++k) {
+    const int tk = k >> 2, qk = k & 3;
+    double sc[T4];
+#pragma unroll
+    for (int t = tk; t < T4; ++t) {
+      const int i = 4 * t + q;
+      double v = (k < i && i < n) ? double(kv[t][k]) : 0.0;
+      if (k == i) v = i < n ? cdiag : 1.0;
+      sc[t] = v;
+    }
+#pragma unroll
+    for (int j = 0; j < k; ++j) {
+      const double lkj = quad_bcast(A[tk][j], qk);  // L_kj from the lane owning row k
+#pragma unroll
+      for (int t = tk; t < T4; ++t) sc[t] = fma(-A[t][j], lkj, sc[t]);
+    }
+    const double sv = sc[tk];
     double y = __builtin_amdgcn_rsq(sv);  // 1/sqrt: v_rsq_f64 + two Newton steps
     y = y * fma(-0.5 * sv, y * y, 1.5);
     y = y * fma(-0.5 * sv, y * y, 1.5);
-    const double ry = quad_bcast(y, qj);
-    const double dj = sv * y;
-    if (q == qj) rin[tj] = y;
+    const double ry = quad_bcast(y, qk);
+    const double dk = sv * y;
+    if (q == qk) rin[tk] = y;
 #pragma unroll
-    for (int t = tj; t < T4; ++t) {
-      const double v = A[t][j] * ry;
-      A[t][j] = t > tj ? v : (q > qj ? v : (q == qj ? dj : 0.0));
-    }
-#pragma unroll
-    for (int k = j + 1; k < NP; ++k) {
-      const double lk = quad_bcast(A[k >> 2][j], k & 3);  // L_kj from the lane owning row k
-#pragma unroll
-      for (int t = k >> 2; t < T4; ++t) {
-        const double lij = (t == tj && q <= qj) ? 0.0 : A[t][j];
-        A[t][k] = fma(-lij, lk, A[t][k]);
-      }
+    for (int t = tk; t < T4; ++t) {
+      const double v = sc[t] * ry;
+      A[t][k] = t > tk ? v : (q > qk ? v : (q == qk ? dk : 0.0));
     }
   }
   // forward: L y = (g, 1)
@@ -1120,7 +1125,10 @@ DEVI void bqp_quad(const Params& p, int tb) {
 #pragma unroll
   for (int t = 0; t < T4; ++t) {
     c2 = fma(bd[t], bd[t], c2);
-    c3 = fma(g[t], bd[t], c3);
+    // g again (re-read, not kept in registers through the factorisation)
+    const int i = 4 * t + q;
+    const double gt = i < n ? br[min(i, n - 1)] * inv_m : 0.0;
+    c3 = fma(gt, bd[t], c3);
   }
   c2 = quad_sum(c2);
   c3 = quad_sum(c3);
@@ -1135,8 +1143,11 @@ DEVI void bqp_quad(const Params& p, int tb) {
 HDI int qp_np(int n) { return n <= 8 ? 8 : (n <= 16 ? 16 : (n <= 24 ? 24 : (n <= 32 ? 32 : (n <= 48 ? 48 : 64)))); }
 constexpr int kQpThreads = 256;  // 64 QPs per workgroup
 
+#ifndef MPCMMD_QP24_OCC
+#define MPCMMD_QP24_OCC 2
+#endif
 template <int NP>
-__global__ __launch_bounds__(kQpThreads) void k_bqp(Params p, int tb) {
+__global__ __launch_bounds__(kQpThreads, NP == 24 ? MPCMMD_QP24_OCC : 1) void k_bqp(Params p, int tb) {
   bqp_quad<NP>(p, tb);
 }
 
