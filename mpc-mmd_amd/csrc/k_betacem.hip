@@ -1642,14 +1642,15 @@ void launch_bsample(const Params& p, int tb, hipStream_t s) {
   hipLaunchKernelGGL(k_bsample, dim3(p.nb), dim3(64 * kSampleWaves), 0, s, p, tb);
 }
 
-// waves per candidate: ~8 single-wave workgroups per SIMD over the launch
+// waves per candidate: ~16 single-wave workgroups per SIMD over the launch
+// (16 per candidate at B = 1024: 8 -> 16 measured -8.5%)
 int sel_waves(int nb) {
   static const int env = [] {
     const char* e = std::getenv("MPCMMD_SEL_WAVES");  // experiments: waves per candidate
     return e ? std::atoi(e) : 0;
   }();
   if (env > 0) return env;
-  return std::max(4, std::min(25, 8192 / std::max(1, nb)));
+  return std::max(4, std::min(25, 16384 / std::max(1, nb)));
 }
 
 template <int NQ>
