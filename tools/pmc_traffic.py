@@ -22,7 +22,7 @@ def per_kernel(path, counter):
         name = r["Kernel_Name"]
         if "k_" not in name:
             continue
-        short = name[name.find("k_") + 2:].split("(")[0]
+        short = name[name.find("k_") + 2:].split("(")[0].split("<")[0]
         tot[short] += float(r["Counter_Value"])
         cnt[short] += 1
     return {k: tot[k] / cnt[k] for k in tot}
