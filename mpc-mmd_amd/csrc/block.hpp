@@ -49,6 +49,35 @@ DEVI void bitonic_sort(unsigned long long* k, int N) {
   __syncthreads();
 }
 
+// The same network with one key per thread (N <= blockDim.x): the stages
+// whose partner is in the same wave (stride < 64) exchange by lane shuffles,
+// only the wider ones go through LDS with barriers (10 of 55 stages at
+// N = 1024).  Same compare-exchanges, so the same result as bitonic_sort.
+DEVI void bitonic_sort_reg(unsigned long long* k, int N) {
+  const int i = threadIdx.x;
+  __syncthreads();
+  unsigned long long a = i < N ? k[i] : ~0ull;
+  for (int size = 2; size <= N; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      unsigned long long b;
+      if (stride >= 64) {
+        __syncthreads();
+        if (i < N) k[i] = a;
+        __syncthreads();
+        b = i < N ? k[i ^ stride] : ~0ull;
+      } else {
+        b = __shfl_xor(a, stride, 64);
+      }
+      const bool up = (i & size) == 0, lower = (i & stride) == 0;
+      const unsigned long long mn = a < b ? a : b, mx = a < b ? b : a;
+      a = lower == up ? mn : mx;
+    }
+  }
+  __syncthreads();
+  if (i < N) k[i] = a;
+  __syncthreads();
+}
+
 struct ReduceScratch {
   double d[16];
   int i[16];

@@ -77,6 +77,18 @@ DEVI double dpp_d(double v) {
   const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), CTRL, ROWS, 0xF, false);
   return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
 }
+// v_permlane32_swap (W = 32): lanes 32-63 of x <-> lanes 0-31 of y;
+// v_permlane16_swap (W = 16): the odd 16-lane rows of x <-> the even rows of y.
+// Inline asm: hipcc (ROCm 7.2) may commute the builtins' two operands, which
+// exchanges the other halves.  s_nop 1: the VALU-write -> permlane hazard.
+template <int W>
+DEVI void permlane_swap(float& x, float& y) {
+  if constexpr (W == 32)
+    __asm__ volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+  else
+    __asm__ volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+
 // sum of the 64 lanes, wave-uniform result (VALU only: quad / row butterflies,
 // then the row broadcasts into lane 63)
 DEVI int wave_total(int v) {
@@ -178,6 +190,10 @@ constexpr int kDistThreads = 256;
 // hit that XCD's L2, instead of once per tile.
 constexpr int kXcds = 8;
 
+// The matrix is symmetric and |a - b| == |b - a| exactly, so a tile of rows
+// computes only the columns from its own first row on and also writes the
+// mirrored entries D[j][r0 .. r0 + 31] of every later column j (eight
+// float4 per thread): half the VALU work of the full matrix, same bits.
 __global__ __launch_bounds__(kDistThreads) void k_bdist(Params p) {
   __shared__ __attribute__((aligned(16))) float Fr[kDistRows][kF + 2];
   const int M = p.M, Md = dist_stride(M), T = (M + kDistRows - 1) / kDistRows;
@@ -192,18 +208,32 @@ __global__ __launch_bounds__(kDistThreads) void k_bdist(Params p) {
   }
   __syncthreads();
   const int rn = min(kDistRows, M - r0);
-  float* D = p.bdist + (size_t(b) * M + r0) * Md;
-  for (int j = tid; j < Md; j += kDistThreads) {
+  float* Db = p.bdist + size_t(b) * M * Md;
+  float* D = Db + size_t(r0) * Md;
+  for (int j = r0 + tid; j < Md; j += kDistThreads) {
     float fj[kF];
     const int jc = min(j, M - 1);
 #pragma unroll
     for (int f = 0; f < kF; ++f) fj[f] = Fg[f * M + jc];
-    for (int r = 0; r < rn; ++r) {
-      const float* fr = Fr[r];  // wave-uniform: LDS broadcast
-      float d = fabsf(fr[0] - fj[0]);
+    // a later real column: its row gets this tile's 32 entries (the tile is
+    // full: a later column exists only if r0 + 32 < M)
+    const bool mirror = j >= r0 + kDistRows && j < M;
+    float4* dst = reinterpret_cast<float4*>(Db + size_t(mirror ? j : 0) * Md + r0);
+    for (int rg = 0; rg < kDistRows / 4; ++rg) {
+      float dv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int f = 1; f < kF; ++f) d = d + fabsf(fr[f] - fj[f]);
-      D[size_t(r) * Md + j] = j < M ? d : __builtin_inff();
+      for (int rr = 0; rr < 4; ++rr) {
+        const int r = 4 * rg + rr;
+        if (r < rn) {
+          const float* fr = Fr[r];  // wave-uniform: LDS broadcast
+          float d = fabsf(fr[0] - fj[0]);
+#pragma unroll
+          for (int f = 1; f < kF; ++f) d = d + fabsf(fr[f] - fj[f]);
+          D[size_t(r) * Md + j] = j < M ? d : __builtin_inff();
+          dv[rr] = d;
+        }
+      }
+      if (mirror) dst[rg] = make_float4(dv[0], dv[1], dv[2], dv[3]);
     }
   }
 }
@@ -464,6 +494,7 @@ constexpr int kSampleTiles = kBzCols / 16;  // 6 tiles of 16 sample columns (89 
 constexpr int kTilesPerWave = MPCMMD_SAMPLE_TILES;
 constexpr int kSampleWaves = kSampleTiles / kTilesPerWave;
 static_assert(kSampleTiles % kTilesPerWave == 0, "tiles per wave");
+static_assert(kTilesPerWave % 2 == 0, "sample tiles are loaded in pairs");
 static_assert(kBzCols >= kNew, "sample tiles");
 
 DEVI d4 mfma64(double a, double b, d4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
@@ -478,7 +509,7 @@ struct SampleBlock {
   double uX[3];  // U[p0 + r][4i + h]        (B of W U^T, A of U S)
   double L;      // L_jj of position p0 + r
   double m[4];   // mean of position p0 + h + 4i
-  double z[kTilesPerWave][4];  // Z[p0 + 4k + h][s0 + 16t + r]
+  double z[kTilesPerWave][4];  // Z[p0 + 4k + h][sample of (tile t, lane r)] (sample_of)
 };
 
 DEVI void load_block(SampleBlock& q, const double* G, const double* gm, const double* z, int p0, int s0, int r,
@@ -494,10 +525,16 @@ DEVI void load_block(SampleBlock& q, const double* G, const double* gm, const do
   q.L = g[kGenL];
 #pragma unroll
   for (int i = 0; i < 4; ++i) q.m[i] = gm[p0 + h + 4 * i];
+  // tiles in pairs: lane r of tiles 2u, 2u + 1 takes samples 32u + 2r, 32u +
+  // 2r + 1, so one 16-byte load fetches both B operands
 #pragma unroll
-  for (int t = 0; t < kTilesPerWave; ++t)
+  for (int u = 0; u < kTilesPerWave / 2; ++u)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) q.z[t][k] = z[size_t(p0 + 4 * k + h) * kBzCols + s0 + 16 * t + r];
+    for (int k = 0; k < 4; ++k) {
+      const double2 zz = *reinterpret_cast<const double2*>(z + size_t(p0 + 4 * k + h) * kBzCols + s0 + 32 * u + 2 * r);
+      q.z[2 * u][k] = zz.x;
+      q.z[2 * u + 1][k] = zz.y;
+    }
 }
 
 // One block's MFMAs for the wave's tiles, all accumulating in place:
@@ -533,12 +570,23 @@ DEVI void block_mfma(const SampleBlock& cur, d4* S, d4* Y, int r, int h) {
 }
 
 // the finished block's samples to fp32 (the sigma coordinate M clipped)
+// Register i of lane row h holds position p0 + h + 4i; a 4 x 4 transpose
+// across (lane row, register) -- a block swap by permlane32, then the 2 x 2
+// blocks by permlane16 -- leaves positions p0 + 4h .. p0 + 4h + 3 in lane row
+// h, stored as one 16-byte write per tile.
 DEVI void block_store(const d4* Yv, float* Y, int p0, int M, int ys, int h) {
 #pragma unroll
   for (int t = 0; t < kTilesPerWave; ++t) {
-    float* yrow = Y + size_t(16 * t) * ys + p0 + h;
+    float v[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) yrow[4 * i] = p0 + h + 4 * i == M ? fmaxf(float(Yv[t][i]), 0.01f) : float(Yv[t][i]);
+    for (int i = 0; i < 4; ++i) v[i] = p0 + h + 4 * i == M ? fmaxf(float(Yv[t][i]), 0.01f) : float(Yv[t][i]);
+    permlane_swap<32>(v[0], v[2]);
+    permlane_swap<32>(v[1], v[3]);
+    permlane_swap<16>(v[0], v[1]);
+    permlane_swap<16>(v[2], v[3]);
+    // sample s0 + 32 (t / 2) + 2 r + t % 2
+    float4* yrow = reinterpret_cast<float4*>(Y + size_t(32 * (t >> 1) + (t & 1)) * ys + p0 + 4 * h);
+    *yrow = make_float4(v[0], v[1], v[2], v[3]);
   }
 }
 
@@ -552,7 +600,7 @@ __global__ __launch_bounds__(64 * kSampleWaves) void k_bsample(Params p, int tb)
   const double* gm = p.genm + size_t(b) * Pp;
   const double* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
   const int ys = ygen_stride(M);
-  float* Y = p.ygen + (size_t(b) * kBzCols + s0 + r) * ys;
+  float* Y = p.ygen + (size_t(b) * kBzCols + s0 + 2 * r) * ys;
   d4 S[kTilesPerWave], Ya[kTilesPerWave], Yb[kTilesPerWave];
 #pragma unroll
   for (int t = 0; t < kTilesPerWave; ++t) S[t] = d4{0.0, 0.0, 0.0, 0.0};
@@ -693,18 +741,6 @@ int ker_waves(int M, int n) {
 constexpr float kNegLog2e = -1.44269504088896340736f;
 
 DEVI float dpp_f_ror8(float v) { return __int_as_float(dpp_i<0x128>(__float_as_int(v))); }
-
-// v_permlane32_swap (W = 32): lanes 32-63 of x <-> lanes 0-31 of y;
-// v_permlane16_swap (W = 16): the odd 16-lane rows of x <-> the even rows of y.
-// Inline asm: hipcc (ROCm 7.2) may commute the builtins' two operands, which
-// exchanges the other halves.  s_nop 1: the VALU-write -> permlane hazard.
-template <int W>
-DEVI void permlane_swap(float& x, float& y) {
-  if constexpr (W == 32)
-    __asm__ volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
-  else
-    __asm__ volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
-}
 
 // v[j] per lane -> lanes 8 j + 4..7 hold the 64-lane sum of v[j] (row_ror:4
 // moves lane i - 4 into lane i, so the 8-lane group's total lands in its upper quad)

@@ -17,6 +17,13 @@ namespace mpcmmd {
 
 namespace {
 
+// Intra-wave LDS hand-off: one wave's LDS operations execute in order, so
+// only the compiler must be kept from reordering them.
+DEVI void wave_sync_lds() {
+  __builtin_amdgcn_wave_barrier();
+  __asm__ volatile("" ::: "memory");
+}
+
 constexpr int kMaxSortN = 4096;
 constexpr int kN = 100;
 
@@ -28,6 +35,7 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
   __shared__ int cem5[kElite];
   __shared__ float pe[kElite][8];
   __shared__ double L[8][8];
+  __shared__ double cvs[8][8];
   __shared__ float mean32[8];
   __shared__ int imin_s;
   const int B = p.B;
@@ -40,7 +48,8 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
   // ---- argsort(res_norm), stable ------------------------------------------
   for (int i = tid; i < N; i += blockDim.x)
     keys[i] = i < B ? ((unsigned long long)sort_key(p.res_norm[g0 + i]) << 32) | unsigned(i) : ~0ull;
-  bitonic_sort(keys, N);
+  if (N <= int(blockDim.x)) bitonic_sort_reg(keys, N);
+  else bitonic_sort(keys, N);
   for (int i = tid; i < B; i += blockDim.x) {
     perm[i] = int(keys[i] & 0xFFFFFFFFu);
     cf.tr_proj[size_t(t) * B + i] = perm[i];
@@ -49,7 +58,8 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
   // ---- argsort(obs cost) over the permuted batch -------------------------
   for (int i = tid; i < N; i += blockDim.x)
     keys[i] = i < B ? ((unsigned long long)sort_key(p.obs_cost[g0 + perm[i]]) << 32) | unsigned(i) : ~0ull;
-  bitonic_sort(keys, N);
+  if (N <= int(blockDim.x)) bitonic_sort_reg(keys, N);
+  else bitonic_sort(keys, N);
   if (tid < kEliteCost) {
     const int e = perm[int(keys[tid] & 0xFFFFFFFFu)];
     el[tid] = e;  // candidate index within the configuration
@@ -138,8 +148,10 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
     pe[q][c] = pop[size_t(el[cem5[q]]) * 8 + c];
   }
   __syncthreads();
-  // ---- compute_shifted_samples (fp64) on thread 0 --------------------------
-  if (tid == 0) {
+  // ---- compute_shifted_samples (fp64): weights per thread, mean entry c on
+  // thread c, covariance entry (a, c) on thread 8 a + c (each sum in the
+  // reference's order), the 8x8 Cholesky on thread 0
+  if (tid < 64) {
     double c5[kElite], wgt[kElite];
     for (int q = 0; q < kElite; ++q) c5[q] = double(cost20[cem5[q]]);
     double cmin = c5[0];
@@ -149,32 +161,32 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
       wgt[q] = exp(-(1.0 / 0.9) * (c5[q] - cmin));
       sw += wgt[q];
     }
-    float m32[8];
-    for (int c = 0; c < 8; ++c) {
+    if (tid < 8) {
+      const int c = tid;
       double s = 0.0;
       for (int q = 0; q < kElite; ++q) s += wgt[q] * double(pe[q][c]);
-      m32[c] = float((1.0 - 0.6) * double(cf.mean[c]) + 0.6 * s / sw);
-      mean32[c] = m32[c];
+      mean32[c] = float((1.0 - 0.6) * double(cf.mean[c]) + 0.6 * s / sw);
     }
-    double cv[8][8];
-    for (int a = 0; a < 8; ++a)
-      for (int c = 0; c < 8; ++c) {
-        double s = 0.0;
-        for (int q = 0; q < kElite; ++q)
-          s += wgt[q] * (double(pe[q][a]) - double(m32[a])) * (double(pe[q][c]) - double(m32[c]));
-        const float v = float((1.0 - 0.6) * double(cf.cov[a * 8 + c]) + 0.6 * s / sw + (a == c ? 0.01 : 0.0));
-        cv[a][c] = double(v);
-        cf.cov[a * 8 + c] = v;
-      }
-    for (int c = 0; c < 8; ++c) cf.mean[c] = m32[c];
+    wave_sync_lds();
+    const int a = tid >> 3, c = tid & 7;
+    const double ma = double(mean32[a]), mc = double(mean32[c]);
+    double s = 0.0;
+    for (int q = 0; q < kElite; ++q) s += wgt[q] * (double(pe[q][a]) - ma) * (double(pe[q][c]) - mc);
+    const float v = float((1.0 - 0.6) * double(cf.cov[a * 8 + c]) + 0.6 * s / sw + (a == c ? 0.01 : 0.0));
+    cvs[a][c] = double(v);
+    cf.cov[a * 8 + c] = v;
+    if (tid < 8) cf.mean[tid] = mean32[tid];
+    wave_sync_lds();
+  }
+  if (tid == 0) {
     // Cholesky (lower) of the fp32 covariance, in fp64
     for (int j = 0; j < 8; ++j) {
-      double d = cv[j][j];
+      double d = cvs[j][j];
       for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k];
       d = sqrt(d);
       L[j][j] = d;
       for (int i = j + 1; i < 8; ++i) {
-        double s = cv[i][j];
+        double s = cvs[i][j];
         for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k];
         L[i][j] = s / d;
       }
@@ -182,11 +194,13 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
     }
     // idx_min = argmin(cost_batch_temp) (== 0 unless NaN; jnp.argmin: first NaN)
     int im = 0;
-    for (int q = 0; q < kElite; ++q)
-      if (c5[q] != c5[q]) {
+    for (int q = 0; q < kElite; ++q) {
+      const float cq = cost20[cem5[q]];
+      if (cq != cq) {
         im = q;
         break;
       }
+    }
     imin_s = im;
     for (int q = 0; q < kElite; ++q) cf.tr_cem[size_t(t) * kElite + q] = cem5[q];
   }
