@@ -192,10 +192,15 @@ constexpr int kXcds = 8;
 
 // The matrix is symmetric and |a - b| == |b - a| exactly, so a tile of rows
 // computes only the columns from its own first row on and also writes the
-// mirrored entries D[j][r0 .. r0 + 31] of every later column j (eight
-// float4 per thread): half the VALU work of the full matrix, same bits.
+// mirrored entries D[j][r0 .. r0 + 31] of every later column j: half the
+// VALU work of the full matrix, same bits.  The mirrored 32-entry pieces go
+// through LDS, so each store instruction writes whole 128-byte rows (eight
+// lanes per row) instead of 16 bytes to 64 rows.
+constexpr int kMirrorPitch = kDistRows + 4;  // floats per staged row (16-byte aligned, spreads banks)
+
 __global__ __launch_bounds__(kDistThreads) void k_bdist(Params p) {
   __shared__ __attribute__((aligned(16))) float Fr[kDistRows][kF + 2];
+  __shared__ __attribute__((aligned(16))) float Tm[kDistThreads * kMirrorPitch];
   const int M = p.M, Md = dist_stride(M), T = (M + kDistRows - 1) / kDistRows;
   const int L = blockIdx.x, q = L / kXcds;
   const int b = (q / T) * kXcds + L % kXcds, r0 = (q % T) * kDistRows;
@@ -210,31 +215,40 @@ __global__ __launch_bounds__(kDistThreads) void k_bdist(Params p) {
   const int rn = min(kDistRows, M - r0);
   float* Db = p.bdist + size_t(b) * M * Md;
   float* D = Db + size_t(r0) * Md;
-  for (int j = r0 + tid; j < Md; j += kDistThreads) {
-    float fj[kF];
-    const int jc = min(j, M - 1);
+  // a later real column exists only if this tile is full (r0 + 32 < M)
+  for (int j0 = r0; j0 < Md; j0 += kDistThreads) {  // wave-uniform trip count
+    const int j = j0 + tid;
+    if (j < Md) {
+      float fj[kF];
+      const int jc = min(j, M - 1);
 #pragma unroll
-    for (int f = 0; f < kF; ++f) fj[f] = Fg[f * M + jc];
-    // a later real column: its row gets this tile's 32 entries (the tile is
-    // full: a later column exists only if r0 + 32 < M)
-    const bool mirror = j >= r0 + kDistRows && j < M;
-    float4* dst = reinterpret_cast<float4*>(Db + size_t(mirror ? j : 0) * Md + r0);
-    for (int rg = 0; rg < kDistRows / 4; ++rg) {
-      float dv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      for (int f = 0; f < kF; ++f) fj[f] = Fg[f * M + jc];
+      for (int rg = 0; rg < kDistRows / 4; ++rg) {
+        float dv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int r = 4 * rg + rr;
-        if (r < rn) {
-          const float* fr = Fr[r];  // wave-uniform: LDS broadcast
-          float d = fabsf(fr[0] - fj[0]);
+        for (int rr = 0; rr < 4; ++rr) {
+          const int r = 4 * rg + rr;
+          if (r < rn) {
+            const float* fr = Fr[r];  // wave-uniform: LDS broadcast
+            float d = fabsf(fr[0] - fj[0]);
 #pragma unroll
-          for (int f = 1; f < kF; ++f) d = d + fabsf(fr[f] - fj[f]);
-          D[size_t(r) * Md + j] = j < M ? d : __builtin_inff();
-          dv[rr] = d;
+            for (int f = 1; f < kF; ++f) d = d + fabsf(fr[f] - fj[f]);
+            D[size_t(r) * Md + j] = j < M ? d : __builtin_inff();
+            dv[rr] = d;
+          }
         }
+        *reinterpret_cast<float4*>(&Tm[tid * kMirrorPitch + 4 * rg]) = make_float4(dv[0], dv[1], dv[2], dv[3]);
       }
-      if (mirror) dst[rg] = make_float4(dv[0], dv[1], dv[2], dv[3]);
     }
+    __syncthreads();
+    // rows j0 + c (c < 256) of the mirror: 8 lanes per row, 16 bytes each
+    for (int i = tid; i < kDistThreads * (kDistRows / 4); i += kDistThreads) {
+      const int c = i >> 3, part = i & 7, jj = j0 + c;
+      if (jj >= r0 + kDistRows && jj < M)
+        *reinterpret_cast<float4*>(Db + size_t(jj) * Md + r0 + 4 * part) =
+            *reinterpret_cast<const float4*>(&Tm[c * kMirrorPitch + 4 * part]);
+    }
+    __syncthreads();
   }
 }
 
