@@ -1121,40 +1121,37 @@ DEVI void bqp_quad(const Params& p, int tb) {
       a2[t] = fma(-lij, b2, a2[t]);
     }
   }
-  // backward: L^T x = y (x overwrites y row by row, last row first)
-#pragma unroll
-  for (int j = NP - 1; j >= 0; --j) {
-    const int tj = j >> 2, qj = j & 3;
-    double p1 = 0.0, p2 = 0.0;
-#pragma unroll
-    for (int t = tj; t < T4; ++t) {
-      const double lij = (t == tj && q <= qj) ? 0.0 : A[t][j];
-      p1 = fma(lij, a1[t], p1);
-      p2 = fma(lij, a2[t], p2);
-    }
-    p1 = quad_sum(p1);
-    p2 = quad_sum(p2);
-    if (q == qj) {
-      a1[tj] = (a1[tj] - p1) * rin[tj];
-      a2[tj] = (a2[tj] - p2) * rin[tj];
-    }
-  }
+  // C^-1 = L^-T L^-1, so with y1 = L^-1 g, y2 = L^-1 1: sum x1 = y2 . y1,
+  // sum x2 = |y2|^2 and beta = L^-T (y1 + alpha y2) -- one backward sweep
   double s1 = 0.0, s2 = 0.0;
 #pragma unroll
-  for (int t = 0; t < T4; ++t) {
-    if (4 * t + q < n) {
-      s1 += a1[t];
-      s2 += a2[t];
-    }
+  for (int t = 0; t < T4; ++t) {  // padding rows hold y = 0
+    s1 = fma(a2[t], a1[t], s1);
+    s2 = fma(a2[t], a2[t], s2);
   }
   s1 = quad_sum(s1);
   s2 = quad_sum(s2);
   const double alpha = (1.0 - s1) / s2;
+#pragma unroll
+  for (int t = 0; t < T4; ++t) a1[t] = fma(alpha, a2[t], a1[t]);
+  // backward: L^T beta = y1 + alpha y2 (beta overwrites it row by row, last row first)
+#pragma unroll
+  for (int j = NP - 1; j >= 0; --j) {
+    const int tj = j >> 2, qj = j & 3;
+    double p1 = 0.0;
+#pragma unroll
+    for (int t = tj; t < T4; ++t) {
+      const double lij = (t == tj && q <= qj) ? 0.0 : A[t][j];
+      p1 = fma(lij, a1[t], p1);
+    }
+    p1 = quad_sum(p1);
+    if (q == qj) a1[tj] = (a1[tj] - p1) * rin[tj];
+  }
   float bf[T4];
   double bd[T4];
 #pragma unroll
   for (int t = 0; t < T4; ++t) {
-    bf[t] = 4 * t + q < n ? float(a1[t] + alpha * a2[t]) : 0.0f;
+    bf[t] = 4 * t + q < n ? float(a1[t]) : 0.0f;
     bd[t] = double(bf[t]);
   }
   // cost = |L^T beta|^2 - delta |beta|^2 - 2 g^T beta
@@ -1197,7 +1194,7 @@ constexpr int kQpThreads = 256;  // 64 QPs per workgroup
 #define MPCMMD_QP24_OCC 2
 #endif
 template <int NP>
-__global__ __launch_bounds__(kQpThreads, NP == 24 ? MPCMMD_QP24_OCC : 1) void k_bqp(Params p, int tb) {
+__global__ __launch_bounds__(kQpThreads, NP == 24 ? MPCMMD_QP24_OCC : (NP == 16 ? 3 : 1)) void k_bqp(Params p, int tb) {
   bqp_quad<NP>(p, tb);
 }
 
@@ -1529,41 +1526,59 @@ __global__ __launch_bounds__(64) void k_bgen(Params p) {
       A[sym11(a, c)] = s;
     }
   const int j0 = blk * 16, j1 = min(M1, j0 + 16);
-  double u[11], un[11];
+  // u of the block's positions in groups of four, the next group's loads in
+  // flight while one group is processed (one memory latency per block, not
+  // one per position; positions past the block end re-read the last one)
+  auto load4 = [&](double (&uu)[4][11], int grp) {
 #pragma unroll
-  for (int a = 0; a < 11; ++a) u[a] = gen[size_t(j0) * kGenStride + kGenU + a];
-  for (int j = j0; j < j1; ++j) {
-    const int jn = min(j + 1, j1 - 1);  // the next position's u in flight meanwhile
+    for (int jj = 0; jj < 4; ++jj) {
+      const int jc = min(j0 + 4 * grp + jj, j1 - 1);
 #pragma unroll
-    for (int a = 0; a < 11; ++a) un[a] = gen[size_t(jn) * kGenStride + kGenU + a];
-    double v[11];
-#pragma unroll
-    for (int a = 0; a < 11; ++a) {
-      double s = 0.0;
-#pragma unroll
-      for (int c = 0; c < 11; ++c) s = fma(A[sym11i(a, c)], u[c], s);
-      v[a] = s;
+      for (int a = 0; a < 11; ++a) uu[jj][a] = gen[size_t(jc) * kGenStride + kGenU + a];
     }
-    double uv = 0.0;
+  };
+  auto step4 = [&](const double (&uu)[4][11], int grp) {
 #pragma unroll
-    for (int a = 0; a < 11; ++a) uv = fma(u[a], v[a], uv);
-    const double ljj = sqrt(kRidge + uv);
-    const double rl = 1.0 / ljj;
-    double* g = gen + size_t(j) * kGenStride;
-    double w[11];
+    for (int jj = 0; jj < 4; ++jj) {
+      const int j = j0 + 4 * grp + jj;
+      if (j >= j1) break;
+      const double* u = uu[jj];
+      double v[11];
 #pragma unroll
-    for (int a = 0; a < 11; ++a) {
-      w[a] = v[a] * rl;
-      g[kGenW + a] = w[a];
+      for (int a = 0; a < 11; ++a) {
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < 11; ++c) s = fma(A[sym11i(a, c)], u[c], s);
+        v[a] = s;
+      }
+      double uv = 0.0;
+#pragma unroll
+      for (int a = 0; a < 11; ++a) uv = fma(u[a], v[a], uv);
+      const double ljj = sqrt(kRidge + uv);
+      const double rl = 1.0 / ljj;
+      double* g = gen + size_t(j) * kGenStride;
+      double w[11];
+#pragma unroll
+      for (int a = 0; a < 11; ++a) {
+        w[a] = v[a] * rl;
+        g[kGenW + a] = w[a];
+      }
+      g[kGenL] = ljj;
+#pragma unroll
+      for (int a = 0; a < 11; ++a)
+#pragma unroll
+        for (int c = a; c < 11; ++c) A[sym11(a, c)] = fma(-w[a], w[c], A[sym11(a, c)]);
     }
-    g[kGenL] = ljj;
-#pragma unroll
-    for (int a = 0; a < 11; ++a)
-#pragma unroll
-      for (int c = a; c < 11; ++c) A[sym11(a, c)] = fma(-w[a], w[c], A[sym11(a, c)]);
-#pragma unroll
-    for (int a = 0; a < 11; ++a) u[a] = un[a];
-  }
+  };
+  double ua[4][11], ub[4][11];
+  load4(ua, 0);
+  load4(ub, 1);
+  step4(ua, 0);
+  load4(ua, 2);
+  step4(ub, 1);
+  load4(ub, 3);
+  step4(ua, 2);
+  step4(ub, 3);
 }
 
 // k_bsigma (last beta-iteration only): sigma_best when argmin is a new

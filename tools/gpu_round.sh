@@ -9,4 +9,4 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1 && \
 grep -E "passed|failed" gpurun_out/gpu_tests.log | tail -2 && \
 timeout -k 10 400 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err && \
-bash tools/prof.sh $TAG --extra 0
+MPCMMD_GROUPS=1 bash tools/prof.sh $TAG --extra 0
