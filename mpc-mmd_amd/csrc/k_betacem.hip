@@ -1707,15 +1707,16 @@ void launch_bsample(const Params& p, int tb, hipStream_t s) {
   hipLaunchKernelGGL(k_bsample, dim3(p.nb), dim3(64 * kSampleWaves), 0, s, p, tb);
 }
 
-// waves per candidate: ~16 single-wave workgroups per SIMD over the launch
-// (16 per candidate at B = 1024: 8 -> 16 measured -8.5%)
+// waves per candidate: ~16 single-wave workgroups per SIMD over the launch,
+// at most 16 per candidate (B = 1024: 8 -> 16 measured -8.5%; the 512-candidate
+// groups of the two-stream split: 25 -> 16 +1%)
 int sel_waves(int nb) {
   static const int env = [] {
     const char* e = std::getenv("MPCMMD_SEL_WAVES");  // experiments: waves per candidate
     return e ? std::atoi(e) : 0;
   }();
   if (env > 0) return env;
-  return std::max(4, std::min(25, 16384 / std::max(1, nb)));
+  return std::max(4, std::min(16, 16384 / std::max(1, nb)));
 }
 
 template <int NQ>
