@@ -110,7 +110,10 @@ struct mpcmmd_handle {
     void* d = nullptr;
     if (bytes == 0) bytes = 16;
     HIPC(hipMalloc(&d, bytes));
-    HIPC(hipMemset(d, 0, bytes));
+    // zeroed on the handle's own (non-blocking) stream: a null-stream memset
+    // is not ordered before the constant uploads that follow on this stream
+    // and could land after them
+    HIPC(hipMemsetAsync(d, 0, bytes, stream));
     bufs[name] = {d, bytes};
     return d;
   }
@@ -546,6 +549,8 @@ void mpcmmd_destroy(mpcmmd_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (int g = 0; g < mpcmmd_handle::kMaxGroups; ++g)  // group streams drained before their buffers go
+    if (h->gstream[g]) (void)hipStreamSynchronize(h->gstream[g]);
   for (auto& kv : h->bufs) (void)hipFree(kv.second.first);
   for (auto& pe : h->pending) {
     (void)hipEventDestroy(pe.second.first);
