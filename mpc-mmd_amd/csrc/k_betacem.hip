@@ -1340,7 +1340,12 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
   }
   __syncthreads();
   const int imin = info[1] ? info[0] : elite[0];  // jnp.argmin: first NaN, else first minimum
-  if (tid == 0) p.res_beta[size_t(b) * kBetaIters + tb] = info[1] ? __int_as_float(0x7fc00000) : cst[elite[0]];
+  if (tid == 0) {
+    p.res_beta[size_t(b) * kBetaIters + tb] = info[1] ? __int_as_float(0x7fc00000) : cst[elite[0]];
+    double es = 0.0;  // elite costs in rank order (the parity trace; tests/parity.py)
+    for (int q = 0; q < kBetaElite; ++q) es += double(cst[elite[q]]);
+    p.btrace[size_t(b) * kBetaIters + tb] = float(es);
+  }
   // the elites are samples 0..10 of the next iteration, unchanged: carry
   // their top-n rows, sigma, QP solution and cost there (first_sample)
   if (tb < kBetaIters - 1) {

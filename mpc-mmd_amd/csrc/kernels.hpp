@@ -90,6 +90,8 @@ struct Params {
   float* beta;             // [B][n]
   float* sigma;            // [B]
   float* res_beta;         // [B][20]
+  float* btrace;           // [B][20] sum of the 11 elite QP costs per beta-iteration (parity trace: where two
+                           //         runs of the beta-CEM part, compute_beta.py:133)
   // mmd_opt scratch (beta-CEM, compute_beta.py:93-157)
   float* feat;             // [B][22][M]   mother Bernstein coefficients (cx | cy)
   float* bdist;            // [B][M][dist_stride(M)] L1 distances of the mother features

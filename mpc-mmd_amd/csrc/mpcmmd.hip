@@ -507,6 +507,7 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     p.beta = (float*)h->alloc("beta", BT * h->n * 4);
     p.sigma = (float*)h->alloc("sigma", BT * 4);
     p.res_beta = (float*)h->alloc("res_beta", BT * kBetaIters * 4);
+    p.btrace = (float*)h->alloc("btrace", BT * kBetaIters * 4);
     p.dbg = (unsigned long long*)h->alloc("dbg", 64 * 8);
     p.stats = (unsigned long long*)h->alloc("stats", 8 * 8);
     p.wgt = (unsigned long long*)h->alloc("wgt", BT * 8 * 2 * 8);

@@ -20,10 +20,13 @@ writes ``stats/<noise>_noise/noise_<100 sigma>/ts_<H>/<n>_samples_<O>_obs.npz``
 with the ``coll_*`` keys (:459-464).
 
 Random draws: the reference seeds ``np.random.seed(key)`` per configuration
-and draws with NumPy's multivariate_normal / beta.  Those streams can be
-injected (``draws=``, tests/golden pins them against the reference's own
-functions); without them the library's Philox streams keyed by (key, seed)
-are used.
+and draws with NumPy's multivariate_normal / beta (S/validation.py:42-84).
+By default (``rng="numpy"``) the same NumPy draws are made here on the host
+(``reference_draws``: a ``RandomState(key)`` gives the stream of the seeded
+global generator) and handed to the GPU, so the counts are the reference's
+own (tests/golden pins them).  ``rng="philox"`` (``--rng philox``) uses the
+library's counter-based Philox streams keyed by (key, seed) instead: no host
+work, other numbers.
 """
 from __future__ import annotations
 
@@ -35,6 +38,42 @@ import numpy as np
 from . import _native
 
 NUM_ROLLOUTS = 1000  # _num_batch (validation.py:173)
+RNGS = ("numpy", "philox")
+
+
+def _controls(prob, cx, cy):
+    """compute_controls of a saved optimum, fp64 on the fp32 basis
+    (S/validation.py:122-132, 140-146): acc [101], steer [100]."""
+    cx = np.asarray(cx, np.float64).reshape(-1)
+    cy = np.asarray(cy, np.float64).reshape(-1)
+    xd, xdd = np.dot(prob.Pdot_jax, cx), np.dot(prob.Pddot_jax, cx)
+    yd, ydd = np.dot(prob.Pdot_jax, cy), np.dot(prob.Pddot_jax, cy)
+    v = np.sqrt(xd ** 2 + yd ** 2)
+    v = np.hstack((v, v[-1]))
+    acc = np.diff(v) / prob.t
+    acc = np.hstack((acc, acc[-1]))
+    curv = (ydd * xd - yd * xdd) / ((xd ** 2 + yd ** 2) ** 1.5)
+    return acc, np.arctan(curv * prob.wheel_base)
+
+
+def reference_draws(prob, cx, cy, num_prime, noise, key, num_rollouts=NUM_ROLLOUTS):
+    """The draws of compute_rollout_complete (S/validation.py:42-84) for one
+    saved optimum: np.random.seed(key), then acc / steer noise (gaussian:
+    multivariate_normal; beta: Beta(2|acc|, 5|acc|) and Beta(2|steer| + 1e-5,
+    5|steer| + 1e-5) of the optimum's controls), then the const-noise
+    normals.  Returns [3][R][H] fp64 as mpcmmd_validate takes them."""
+    H, R = int(num_prime), int(num_rollouts)
+    acc, steer = _controls(prob, cx, cy)
+    acc, steer = acc[:H], steer[:H]
+    rs = np.random.RandomState(int(key))
+    if noise == "gaussian":
+        na = rs.multivariate_normal(np.zeros(H), np.eye(H), (R,))
+        ns = rs.multivariate_normal(np.zeros(H), np.eye(H), (R,))
+    else:
+        na = rs.beta(prob.beta_a * np.abs(acc), prob.beta_b * np.abs(acc), (R, H))
+        ns = rs.beta(prob.beta_a * np.abs(steer) + 1e-5, prob.beta_b * np.abs(steer) + 1e-5, (R, H))
+    nc = rs.multivariate_normal(np.zeros(H), np.eye(H), (R,))
+    return np.stack([na, ns, nc])
 
 
 def _tracks(prob, x_obs, y_obs, vx_obs, vy_obs):
@@ -51,37 +90,45 @@ def _tracks(prob, x_obs, y_obs, vx_obs, vy_obs):
 
 
 def compute_stats(prob, cx, cy, init_state, x_obs, y_obs, vx_obs, vy_obs, num_prime, noise_level, noise, num_obs,
-                  key, draws=None, num_rollouts=NUM_ROLLOUTS):
+                  key, draws=None, num_rollouts=NUM_ROLLOUTS, rng="numpy"):
     """S/validation.py:134 (static variant: obstacle state, constant-velocity
     tracks); returns (count, count_lane)."""
     xt, yt = _tracks(prob, [x_obs], [y_obs], [vx_obs], [vy_obs])
     return compute_stats_tracks(prob, cx, cy, init_state, xt[0], yt[0], num_prime, noise_level, noise, num_obs, key,
-                                draws, num_rollouts)
+                                draws, num_rollouts, rng)
 
 
 def compute_stats_tracks(prob, cx, cy, init_state, x_obs_traj, y_obs_traj, num_prime, noise_level, noise, num_obs,
-                         key, draws=None, num_rollouts=NUM_ROLLOUTS):
+                         key, draws=None, num_rollouts=NUM_ROLLOUTS, rng="numpy"):
     """D/validation.py:129 (dynamic variant: the saved [num_obs, 100] QP
     tracks are used as they are); returns (count, count_lane)."""
     c, l = compute_stats_batch(prob, np.atleast_2d(cx), np.atleast_2d(cy), np.atleast_2d(init_state), None, None,
                                None, None, num_prime, noise_level, noise, [key],
                                None if draws is None else np.asarray(draws)[None], num_rollouts,
                                x_obs_traj=np.asarray(x_obs_traj, np.float32).reshape(1, num_obs, 100),
-                               y_obs_traj=np.asarray(y_obs_traj, np.float32).reshape(1, num_obs, 100))
+                               y_obs_traj=np.asarray(y_obs_traj, np.float32).reshape(1, num_obs, 100), rng=rng)
     return int(c[0]), int(l[0])
 
 
 def compute_stats_batch(prob, cx, cy, init_state, x_obs, y_obs, vx_obs, vy_obs, num_prime, noise_level, noise, keys,
-                        draws=None, num_rollouts=NUM_ROLLOUTS, x_obs_traj=None, y_obs_traj=None):
+                        draws=None, num_rollouts=NUM_ROLLOUTS, x_obs_traj=None, y_obs_traj=None, rng="numpy"):
     """All configurations of a results file at once (leading configuration
     axis).  Pass ``x_obs_traj`` / ``y_obs_traj`` [K, O, 100] for the dynamic
     variant (saved tracks); otherwise the tracks are rebuilt from the
-    obstacle states like the static script."""
+    obstacle states like the static script.  Without ``draws`` the
+    reference's NumPy draws are made per configuration (``rng="numpy"``) or
+    the library's Philox streams are used (``rng="philox"``)."""
+    if rng not in RNGS:
+        raise ValueError(f"rng must be one of {RNGS}")
     if x_obs_traj is None:
         xt, yt = _tracks(prob, x_obs, y_obs, vx_obs, vy_obs)
     else:
         xt = np.asarray(x_obs_traj, np.float32).reshape(len(keys), prob.num_obs, 100)
         yt = np.asarray(y_obs_traj, np.float32).reshape(len(keys), prob.num_obs, 100)
+    if draws is None and rng == "numpy":
+        cx2, cy2 = np.atleast_2d(cx), np.atleast_2d(cy)
+        draws = np.stack([reference_draws(prob, cx2[k], cy2[k], num_prime, noise, keys[k], num_rollouts)
+                          for k in range(len(keys))])
     return _native.validate(cx, cy, init_state, xt, yt, keys, num_prime, noise, noise_level,
                             prob.acc_const_noise, prob.steer_const_noise, num_rollouts, prob.variant, draws,
                             device=prob._cfg.device)
@@ -128,7 +175,7 @@ def common_configs(d_cvar, d_mmd_opt, num_obs):
 
 
 def validate_files(prob, d_cvar, d_mmd_opt, noise, noise_level, num_prime, num_obs, variant="static",
-                   stats_fn=None, num_rollouts=NUM_ROLLOUTS):
+                   stats_fn=None, num_rollouts=NUM_ROLLOUTS, rng="numpy"):
     """coll_* arrays of one sweep point (S/validation.py:279-364): both costs'
     optima of every common configuration k, validated with key k.
     ``stats_fn(d, idx, keys)`` -> (count, count_lane) replaces the GPU call
@@ -145,10 +192,11 @@ def validate_files(prob, d_cvar, d_mmd_opt, noise, noise_level, num_prime, num_o
         if variant == "dynamic":
             c, l = compute_stats_batch(prob, g("cx"), g("cy"), g("init_state"), None, None, None, None, num_prime,
                                        noise_level, noise, keys, num_rollouts=num_rollouts,
-                                       x_obs_traj=g("x_obs_traj"), y_obs_traj=g("y_obs_traj"))
+                                       x_obs_traj=g("x_obs_traj"), y_obs_traj=g("y_obs_traj"), rng=rng)
         else:
             c, l = compute_stats_batch(prob, g("cx"), g("cy"), g("init_state"), g("x_obs"), g("y_obs"), g("vx_obs"),
-                                       g("vy_obs"), num_prime, noise_level, noise, keys, num_rollouts=num_rollouts)
+                                       g("vy_obs"), num_prime, noise_level, noise, keys, num_rollouts=num_rollouts,
+                                       rng=rng)
         return np.asarray(c, np.float64), np.asarray(l, np.float64)
 
     c_opt, l_opt = run(d_mmd_opt, [m for _, m in rows])
@@ -171,6 +219,8 @@ def main(argv=None):
     ap.add_argument("--variant", default="static", choices=["static", "dynamic"])
     ap.add_argument("--root", default="./data")
     ap.add_argument("--stats_root", default="./stats")
+    ap.add_argument("--rng", default="numpy", choices=RNGS,
+                    help="numpy: the reference's np.random.seed(k) draws (default); philox: the library's streams")
     a = ap.parse_args(argv)
     from .cem import CEM
     for noise in a.noises:
@@ -185,7 +235,8 @@ def main(argv=None):
                         d_opt, d_cvar = load("mmd_opt"), load("cvar")
                         if a.variant == "static":
                             load("mmd_random")  # the static script requires the file (:243-245), unused
-                        out = validate_files(prob, d_cvar, d_opt, noise, noise_level, num_prime, num_obs, a.variant)
+                        out = validate_files(prob, d_cvar, d_opt, noise, noise_level, num_prime, num_obs, a.variant,
+                                             rng=a.rng)
                         dst = stats_path(a.stats_root, noise, noise_level, num_prime, num_reduced, num_obs)
                         os.makedirs(os.path.dirname(dst), exist_ok=True)
                         np.savez(dst, **out)

@@ -14,31 +14,44 @@ def f32(x):
     return np.asarray(x, dtype=F64).astype(F32)
 
 
-def compute_f_bar_max(prob, x, y, x_obs, y_obs):
-    """``compute_f_bar`` (costs.py:50-60) reduced by max over (obstacle, time)
-    as every caller does (costs.py:177-180, 195, 210-213, 227-230).
+def compute_f_bar(prob, x, y, x_obs, y_obs):
+    """``compute_f_bar`` (costs.py:50-60) per (obstacle, sample, step).
 
-    x, y [..., H]; x_obs, y_obs [O, H] -> costbar [...] fp32.
+    x, y [..., H]; x_obs, y_obs [O, H] -> f_bar [O, ..., H] fp32.
     cost = (-(dx^2)/a^2 - dy^2/b^2) + 1, then max(0, cost).
     """
     a2 = F32(prob.a_obs ** 2)
     b2 = F32(prob.b_obs ** 2)
-    out = np.zeros(x.shape[:-1], F32)
+    out = []
     for o in range(x_obs.shape[0]):
         wc = x - x_obs[o]
         ws = y - y_obs[o]
         c = ((-(wc * wc)) / a2 - (ws * ws) / b2) + F32(1)
-        c = np.maximum(F32(0), c)
+        out.append(np.maximum(F32(0), c))
+    return np.stack(out).astype(F32)
+
+
+def compute_f_bar_max(prob, x, y, x_obs, y_obs):
+    """``compute_f_bar`` reduced by max over (obstacle, time) as every caller
+    does (costs.py:177-180, 195, 210-213, 227-230): costbar [...] fp32."""
+    out = np.zeros(x.shape[:-1], F32)
+    for c in compute_f_bar(prob, x, y, x_obs, y_obs):
         out = np.maximum(out, c.max(axis=-1))
     return out
 
 
-def lane_bar_max(prob, y):
-    """``compute_lane_bar`` (costs.py:62-71) max-reduced over time
-    (costs.py:126-127, 142, 150, 165, 168): returns (lb, ub) [...]."""
-    lb = np.maximum(F32(0), -y + F32(prob.y_lb)).max(axis=-1)
-    ub = np.maximum(F32(0), y - F32(prob.y_ub)).max(axis=-1)
+def lane_bar(prob, y):
+    """``compute_lane_bar`` (costs.py:62-71) per (sample, step): (lb, ub)."""
+    lb = np.maximum(F32(0), -y + F32(prob.y_lb))
+    ub = np.maximum(F32(0), y - F32(prob.y_ub))
     return lb.astype(F32), ub.astype(F32)
+
+
+def lane_bar_max(prob, y):
+    """``compute_lane_bar`` max-reduced over time (costs.py:126-127, 142, 150,
+    165, 168): returns (lb, ub) [...]."""
+    lb, ub = lane_bar(prob, y)
+    return lb.max(axis=-1), ub.max(axis=-1)
 
 
 def quantile_linear(x, q):

@@ -125,26 +125,39 @@ def noisy_controls(prob, acc, steer, draws, t, rows):
     B, H = acc.shape
     n_a, n_s, n_c = draws.roll[t, 0], draws.roll[t, 1], draws.roll[t, 2]
     assert n_c.shape == (rows, H)
-    a = acc[:, None, :]
-    s = steer[:, None, :]
-    if prob.noise == "gaussian":
-        acc_pert = (F32(prob.sigma_acc) * np.abs(a)) * n_a[None]
-        steer_pert = (F32(prob.sigma_steer) * np.abs(s)) * n_s[None]
-    else:
+    nba = nbs = None
+    if prob.noise != "gaussian":
+        a = np.abs(acc[:, None, :])
+        s = np.abs(steer[:, None, :])
         key = iteration_key(draws.idx_mpc, t, draws.seed)
         elem = (np.arange(rows, dtype=np.uint64)[:, None] * np.uint64(H)
                 + np.arange(H, dtype=np.uint64)[None, :])
         elem = np.broadcast_to(elem, (B, rows, H))
-        aa = np.broadcast_to(np.abs(a), (B, rows, H))
-        ss = np.broadcast_to(np.abs(s), (B, rows, H))
+        aa = np.broadcast_to(a, (B, rows, H))
+        ss = np.broadcast_to(s, (B, rows, H))
         nba = beta_draws((F32(prob.beta_a) * aa).astype(F64), (F32(prob.beta_b) * aa).astype(F64),
                          key, STREAM_GAMMA_ACC_A, STREAM_GAMMA_ACC_B, elem)
         nbs = beta_draws((F32(prob.beta_a) * ss).astype(F64), (F32(prob.beta_b) * ss).astype(F64),
                          key, STREAM_GAMMA_STEER_A, STREAM_GAMMA_STEER_B, elem)
-        acc_pert = F32(prob.sigma_acc) * (F32(2) * nba - F32(1))
-        steer_pert = F32(prob.K_steer * prob.sigma_steer) * (F32(2) * nbs - F32(1))
-    acc_n = (a + acc_pert) + prob.acc_const_noise * n_c[None]
-    steer_n = (s + steer_pert) + prob.steer_const_noise * n_c[None]
+    return inject_noise(prob, acc, steer, n_a, n_s, n_c, nba, nbs)
+
+
+def inject_noise(prob, acc, steer, n_a, n_s, n_c, beta_acc=None, beta_steer=None):
+    """The perturbation itself (cem_helper.py:405-443): gaussian
+    ``a + sigma |a| n_a + c_a n_c``; beta ``a + sigma (2 b_a - 1) + c_a n_c``
+    and ``s + K_steer sigma (2 b_s - 1) + c_s n_c`` with the Beta draws given
+    ([B, rows, H]).  acc, steer [B, H]; n_* [rows, H]."""
+    a = acc[:, None, :]
+    s = steer[:, None, :]
+    if prob.noise == "gaussian":
+        acc_pert = (F32(prob.sigma_acc) * np.abs(a)) * np.asarray(n_a, F32)[None]
+        steer_pert = (F32(prob.sigma_steer) * np.abs(s)) * np.asarray(n_s, F32)[None]
+    else:
+        acc_pert = F32(prob.sigma_acc) * (F32(2) * np.asarray(beta_acc, F32) - F32(1))
+        steer_pert = F32(prob.K_steer * prob.sigma_steer) * (F32(2) * np.asarray(beta_steer, F32) - F32(1))
+    n_c = np.asarray(n_c, F32)[None]
+    acc_n = (a + acc_pert) + prob.acc_const_noise * n_c
+    steer_n = (s + steer_pert) + prob.steer_const_noise * n_c
     return acc_n.astype(F32), steer_n.astype(F32)
 
 

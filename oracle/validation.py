@@ -45,7 +45,7 @@ def _beta64(a, b, key, sa, sb, elem):
     sb_ = np.where(b > 0, b, 1.0)
     la = np.where(a < 1.0, ga + ua / sa_, ga)
     lb = np.where(b < 1.0, gb + ub / sb_, gb)
-    with np.errstate(over="ignore"):
+    with np.errstate(over="ignore", invalid="ignore"):   # np.where evaluates both branches
         out = np.where(la > lb, 1.0 / (1.0 + np.exp(lb - la)), np.exp(la - lb) / (np.exp(la - lb) + 1.0))
     lim = np.where(ua * 5.0 > ub * 2.0, 1.0, 0.0)
     return np.where((a == 0.0) & (b == 0.0), lim, out)

@@ -1,18 +1,24 @@
 """Generate tests/golden/mmdopt_n50_ref.npz: the ORACLE's (oracle/, the NumPy
-restatement of the reference) solve of BASELINE configs[0] -- the drop-in
-``CEM(50, 4, 0.1, 20, "gaussian", 0, 0)`` (num_batch 100, M = 2500 mother
-rollouts) on configuration k = 0 of S/main_mpc.py:10-21 -- for two outer
-iterations, from injected draws ``Draws.random(prob,
-np.random.default_rng(SEED))`` that the GPU test regenerates.
+restatement of the reference) solve of BASELINE configs[0]'s shape -- the
+drop-in ``CEM(50, 4, 0.1, 20, "gaussian", 0, 0)`` (num_batch 100, M = 2500
+mother rollouts) -- for two outer iterations, from injected draws
+``Draws.random(prob, np.random.default_rng(SEED))`` that the GPU test
+regenerates.  The four obstacles sit INSIDE the H = 20 (3 s) rollout horizon
+(BLOCK_X / BLOCK_Y: one grazing the ego lane, one on it, two on the other
+lane), so a share of the noisy rollouts collides and the MMD obstacle costs
+separate the candidates (configuration k = 0 of S/main_mpc.py:10-21 places
+every obstacle at x >= 35 m, beyond the horizon: every cost is the MMD floor).
 
 The oracle's beta-CEM at M = 2500 takes ~10 s per candidate and outer
 iteration (a 2501-dim Cholesky per beta-iteration), too slow for a GPU
 test, so its result is precomputed here (8 processes, a few minutes).
 Stored: the result tuple, per iteration the elite index sets and every
 candidate's costs / beta-CEM outputs, and per (iteration, candidate,
-beta-iteration) the relative gaps of the sorted QP costs at the argmin
-(0/1) and at the elite boundary (10/11), so the GPU test can tell a
-near-tie from a real difference without re-running the oracle.
+beta-iteration) the minimum QP cost, the sum of the 11 elite costs (the
+trace the GPU records in ``btrace``) and the relative gaps of the sorted QP
+costs at the argmin (0/1) and at the elite boundary (10/11), so the GPU test
+can tell a near-tie from a real difference without re-running the oracle
+(tests/parity.py: beta_divergence).
 
     python tests/golden/make_mmdopt_n50_golden.py     (no reference access needed)
 """
@@ -25,7 +31,7 @@ for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "mpc-mmd_amd")]
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mpc-mmd_amd"), os.path.join(ROOT, "tests")]
 
 import numpy as np  # noqa: E402
 
@@ -35,6 +41,9 @@ from oracle import costs as C  # noqa: E402
 from oracle import helper as Hh  # noqa: E402
 
 N, O, LEVEL, H, B, T, SEED = 50, 4, 0.1, 20, 100, 2, 5
+BLOCK_X = [13.0, 24.0, 18.0, 30.0]
+BLOCK_Y = [4.4, 1.75, -1.75, -1.75]
+IDX_MPC = 4242
 _G = {}
 
 
@@ -43,15 +52,12 @@ def _init(prob, z0, z):
 
 
 def _one(args):
+    from parity import beta_trace
     cxm, cym = args
     tr = []
     beta, res, sigma, sel = bc.compute_cem(_G["prob"], cxm, cym, _G["z0"], _G["z"], tr)
-    gaps = np.zeros((20, 2))
-    for t, d in enumerate(tr):
-        c = np.sort(np.asarray(d["cost"], np.float64))
-        for j, i in enumerate((0, 10)):
-            gaps[t, j] = abs(c[i + 1] - c[i]) / max(abs(c[i]), 1e-6)
-    return beta, res, sigma, sel, gaps
+    _, esum, gaps = beta_trace(tr)
+    return beta, res, sigma, sel, gaps, esum
 
 
 class ParallelCEM(oracle.CEM):
@@ -62,6 +68,7 @@ class ParallelCEM(oracle.CEM):
         super().__init__(*a, **k)
         self.pool = pool
         self.gaps = []
+        self.esum = []
 
     def candidate_costs(self, cost, st, acc, steer, x_obs, y_obs, draws, t):
         p = self.prob
@@ -77,6 +84,7 @@ class ParallelCEM(oracle.CEM):
         sigma = np.array([o[2] for o in out], np.float32)
         sel = np.stack([o[3] for o in out]).astype(np.int64)
         self.gaps.append(np.stack([o[4] for o in out]))
+        self.esum.append(np.stack([o[5] for o in out]))
         xr = np.take_along_axis(xm, sel[:, :, None], axis=1)
         yr = np.take_along_axis(ym, sel[:, :, None], axis=1)
         cb = C.compute_f_bar_max(p, xr, yr, xo, yo)
@@ -86,11 +94,11 @@ class ParallelCEM(oracle.CEM):
 
 
 def main():
-    from optimizer.sweep import static_obstacles
     probe = oracle.CEM(N, O, LEVEL, H, "gaussian", 0.0, 0.0, num_batch=B, maxiter_cem=T)
     draws = oracle.Draws.random(probe.prob, np.random.default_rng(SEED), idx_mpc=0, with_beta_cem=True)
-    ob = static_obstacles(0, O)
-    xo, yo, _ = Hh.compute_obs_trajectories(probe.prob, ob["x"], ob["y"], ob["vx"], ob["vy"], ob["psi"])
+    z = np.zeros(O)
+    ob = dict(idx_mpc=IDX_MPC)
+    xo, yo, _ = Hh.compute_obs_trajectories(probe.prob, BLOCK_X, BLOCK_Y, z, z, z)
     init = np.array([0.0, 1.75, 5.0, 0.0, 0.0, 0.0], np.float32)
     mean = np.array([15] * 4 + [0] * 4, np.float32)
     cov = np.diag([20.0] * 4 + [100.0] * 4).astype(np.float32)
@@ -101,13 +109,16 @@ def main():
         ref = ora.solve("mmd_opt", ob["idx_mpc"], init, mean, cov, xo, yo, 15.0, draws=draws, trace=trace)
     out = dict(seed=SEED, idx_mpc=ob["idx_mpc"], x_obs=xo, y_obs=yo, init=init, mean=mean, cov=cov,
                cx=ref[0], cy=ref[1], cost_lane=ref[2], cost_obs=ref[3], beta=ref[4], sigma=ref[5], res_beta=ref[6],
-               gaps=np.stack(ora.gaps))
+               gaps=np.stack(ora.gaps), esum=np.stack(ora.esum))
     for t, d in enumerate(trace):
         for key in ("perm", "elite_obs", "elite_cem", "obs", "lane", "res_beta", "sigma", "beta", "res_norm", "cost20"):
             out[f"t{t}_{key}"] = np.asarray(d[key])
     dst = os.path.join(HERE, "mmdopt_n50_ref.npz")
     np.savez_compressed(dst, **out)
     print("wrote", dst, "cost_obs", ref[3], "sigma", ref[5])
+    for t in range(T):
+        o = out[f"t{t}_obs"]
+        print(f"iteration {t}: obs min {o.min():.4f} max {o.max():.4f}, {(o > o.min() + 1e-2).sum()} candidates above the floor")
 
 
 if __name__ == "__main__":

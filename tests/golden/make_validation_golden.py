@@ -22,8 +22,10 @@ namespace provides what the functions read from globals:
     are constant rows;
   * ``_num_batch = 1000`` (S/validation.py:173).
 
-Outputs per case: inputs, the controls, the 1000 x H rollouts and the
-(count, count_lane) the reference computes.  The draws are NumPy's own
+Outputs per case: inputs, the controls, the 1000 x H rollouts, their
+per-element collision residuals f_bar [O][1000][H] and lane bars, and the
+(count, count_lane) the reference computes.  Also the static driver's scenario
+sequence: ``compute_obs_data`` of S/main_mpc.py:10-21 executed for k < 200.  The draws are NumPy's own
 (np.random.seed(key) + multivariate_normal / beta), so the oracle's
 restatement of that call sequence (oracle.validation.draws_numpy) and the
 GPU kernel fed with those draws are pinned to the reference's numbers.
@@ -46,11 +48,11 @@ H = 20          # num_prime
 O = 4           # num_obs
 
 
-def load_functions(path, ns):
+def load_functions(path, ns, names=FUNCS):
     """Execute the named function definitions of a reference script in ns."""
     tree = ast.parse(open(path).read(), path)
-    defs = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name in FUNCS]
-    assert sorted(d.name for d in defs) == sorted(FUNCS), [d.name for d in defs]
+    defs = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name in names]
+    assert sorted(d.name for d in defs) == sorted(names), [d.name for d in defs]
     exec(compile(ast.Module(body=defs, type_ignores=[]), path, "exec"), ns)
     return ns
 
@@ -65,12 +67,12 @@ def reference_basis():
     return P, Pd.astype(np.float32), Pdd.astype(np.float32)
 
 
-def make_prob(variant, acc_c, steer_c, Pd, Pdd):
+def make_prob(variant, acc_c, steer_c, Pd, Pdd, H_=H, O_=O):
     from oracle.helper import compute_obs_trajectories
     from oracle.problem import Problem
     y_lb, y_ub = (-2.25, 2.25) if variant == "static" else (-2.25, -1.25)   # S/opt/cem.py:155, D/opt/cem.py:155
     K_steer = 0.01 if variant == "static" else 0.05                          # cem_helper.py:24
-    ora = Problem(10, O, 0.1, H, "gaussian", acc_c, steer_c, variant=variant)
+    ora = Problem(10, O_, 0.1, H_, "gaussian", acc_c, steer_c, variant=variant)
     helper = types.SimpleNamespace(K_steer=K_steer,
                                    compute_obs_trajectories=lambda *a: compute_obs_trajectories(ora, *a))
     return types.SimpleNamespace(t=15 / 100, wheel_base=2.5, a_obs=4.25, b_obs=2.75, y_lb=y_lb, y_ub=y_ub,
@@ -97,6 +99,93 @@ CASES = [
     ("dynamic_gauss", "dynamic", "gaussian", 0.2, 0.1, 0.02, -1.75, -1.75, 0.8, 7),
     ("dynamic_beta", "dynamic", "beta", 0.3, 0.05, 0.0, -1.75, -1.75, 1.2, 11),
 ]
+
+
+OBS_COUNTS = (2, 4, 9)   # num_obs <= 9: the reference's grid (S/main_mpc.py:13) places at most 9
+OBS_CONFIGS = 200        # S/main_mpc.py:76
+
+
+def obstacle_configs():
+    """The static driver's scenario sequence, executed: for k < 200,
+    ``compute_obs_data(num_obs, k)`` (S/main_mpc.py:10-21) and the
+    ``np.random.randint(1, 10000)`` idx_mpc the driver draws right after it
+    (:114) -> obs_<O>_{x,y,idx} [200][O] / [200]."""
+    ns = load_functions(os.path.join(REF, "synthetic_static_obs", "main_mpc.py"), {"np": np},
+                        names=("compute_obs_data",))
+    out = {}
+    for O_ in OBS_COUNTS:
+        xs, ys, idx = [], [], []
+        for k in range(OBS_CONFIGS):
+            x, y, vx, vy, psi = ns["compute_obs_data"](O_, k)
+            assert not (vx.any() or vy.any() or psi.any())
+            xs.append(x)
+            ys.append(y)
+            idx.append(np.random.randint(1, 10000))
+        out.update({f"obs_{O_}_x": np.array(xs, np.float64), f"obs_{O_}_y": np.array(ys),
+                    f"obs_{O_}_idx": np.array(idx, np.int64)})
+    return out
+
+
+# The validation SCRIPT (S/validation.py:224-464) on small data files of the
+# S/main_mpc.py:130-135 layout: configurations k from compute_obs_data, the
+# cvar file holding k in CVAR_K, the mmd_opt file k in OPT_K (the drivers
+# save only the configurations each cost solved, so the files differ)
+SCRIPT_POINTS = [("gaussian", 0.1), ("beta", 0.3)]
+SCRIPT_H, SCRIPT_O, SCRIPT_N = 50, 4, 10
+CVAR_K = (0, 2, 3, 5, 8, 11)
+OPT_K = (1, 2, 3, 5, 7, 8, 11)
+
+
+def script_cases(P, Pd, Pdd):
+    """For each sweep point: the two data files and the coll_* arrays the
+    reference's main loop computes from them -- the loop of :284-362
+    restated (set intersection, first matching row, key = position k) around
+    the EXECUTED compute_stats."""
+    obs_ns = load_functions(os.path.join(REF, "synthetic_static_obs", "main_mpc.py"), {"np": np},
+                            names=("compute_obs_data",))
+    out = {}
+    for noise, level in SCRIPT_POINTS:
+        prob = make_prob("static", 0.0, 0.0, Pd, Pdd, H_=SCRIPT_H, O_=SCRIPT_O)
+        ns = load_functions(os.path.join(REF, "synthetic_static_obs", "validation.py"),
+                            {"np": np, "prob": prob, "_num_batch": 1000})
+        files = {}
+        for cost, ks in (("cvar", CVAR_K), ("mmd_opt", OPT_K)):
+            d = {key: [] for key in ("cx", "cy", "init_state", "x_obs", "y_obs", "vx_obs", "vy_obs")}
+            for k in ks:
+                x, y, vx, vy, _ = obs_ns["compute_obs_data"](SCRIPT_O, k)
+                # an optimum-like plan per (cost, k): lane change or lane keeping, some acceleration
+                y1 = -1.75 if (k + (cost == "cvar")) % 2 else 1.75
+                cx, cy = saved_optimum(P, 1.75, y1, 0.6 + 0.15 * (k % 5))
+                for key, v in (("cx", cx), ("cy", cy), ("init_state", [0.0, 1.75, 5.0, 0.0, 0.0, 0.0]), ("x_obs", x),
+                               ("y_obs", y), ("vx_obs", vx), ("vy_obs", vy)):
+                    d[key].append(np.asarray(v, np.float64))
+            files[cost] = {key: np.array(v) for key, v in d.items()}
+        mat = lambda d: np.hstack((d["init_state"], d["x_obs"][:, 0:SCRIPT_O], d["y_obs"][:, 0:SCRIPT_O],
+                                   d["vx_obs"][:, 0:SCRIPT_O], d["vy_obs"][:, 0:SCRIPT_O]))
+        cvar_matrix, opt_matrix = mat(files["cvar"]), mat(files["mmd_opt"])
+        cset = set([tuple(x) for x in cvar_matrix])
+        dset = set([tuple(x) for x in opt_matrix])
+        eset = np.array([x for x in cset & dset])
+        coll = {key: [] for key in ("coll_cvar", "coll_cvar_lane", "coll_mmd_opt", "coll_mmd_opt_lane")}
+        for k in range(eset.shape[0]):
+            for cost, m in (("mmd_opt", opt_matrix), ("cvar", cvar_matrix)):
+                i = np.where(np.all(eset[k] == m, axis=1))[0]
+                if len(i) > 1:
+                    i = i[0]
+                f = files[cost]
+                c, cl = ns["compute_stats"](f["cx"][i], f["cy"][i], f["init_state"][i], f["x_obs"][i], f["y_obs"][i],
+                                            f["vx_obs"][i], f["vy_obs"][i], SCRIPT_H, level, noise, SCRIPT_O, k)[:2]
+                coll[f"coll_{cost}"] = np.append(coll[f"coll_{cost}"], c)
+                coll[f"coll_{cost}_lane"] = np.append(coll[f"coll_{cost}_lane"], cl)
+        pre = f"script_{noise}_"
+        for cost, f in files.items():
+            out.update({pre + cost + "_" + key: v for key, v in f.items()})
+        out.update({pre + key: np.asarray(v, np.float64) for key, v in coll.items()})
+        print(f"script {noise}: {eset.shape[0]} common configurations, coll_cvar {coll['coll_cvar']}, "
+              f"coll_mmd_opt {coll['coll_mmd_opt']}")
+    out.update(script_points=np.array([p[0] for p in SCRIPT_POINTS]), script_levels=np.array([p[1] for p in SCRIPT_POINTS]),
+               script_num_prime=SCRIPT_H, script_num_obs=SCRIPT_O, script_num_reduced=SCRIPT_N)
+    return out
 
 
 def main():
@@ -137,6 +226,10 @@ def main():
             yt = (yo[:, None] + vy[:, None] * tt).astype(np.float32)
             res = ns["compute_stats"](cx, cy, init, xt, yt, H, level, noise, O, key)
         count, count_lane, x_roll, y_roll = res[:4]
+        # the reference's per-element residuals of those rollouts (what
+        # compute_stats counts): f_bar [O][R][H], lane bars [R][H]
+        f_bar = ns["compute_f_bar_temp"](np.asarray(xt, np.float64), np.asarray(yt, np.float64), x_roll, y_roll, H, O)
+        lane_lb, lane_ub = ns["compute_lane_bar"](y_roll, H)
         print(f"{name}: count {count} count_lane {count_lane}")
         assert 0 < count < 1000, "the case should collide for some rollouts only"
         pre = name + "_"
@@ -146,7 +239,10 @@ def main():
                     pre + "vy_obs": vy, pre + "x_obs_traj": np.asarray(xt, np.float32),
                     pre + "y_obs_traj": np.asarray(yt, np.float32), pre + "acc": acc, pre + "steer": steer,
                     pre + "x_roll": x_roll, pre + "y_roll": y_roll, pre + "count": int(count),
-                    pre + "count_lane": int(count_lane)})
+                    pre + "count_lane": int(count_lane), pre + "f_bar": f_bar, pre + "lane_lb": lane_lb,
+                    pre + "lane_ub": lane_ub})
+    out.update(obstacle_configs())
+    out.update(script_cases(P, Pd, Pdd))
     dst = os.path.join(here, "validation_ref.npz")
     np.savez_compressed(dst, **out)
     print("wrote", dst)

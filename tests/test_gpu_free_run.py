@@ -5,19 +5,25 @@ lane inside the rollout horizon, so the optimum is not trivial (collisions
 are possible and the CEM has to steer around them).
 
 Per outer iteration the GPU's per-candidate costs and elite index sets are
-read back and compared with the oracle's trace.  The two runs must agree to
-the end -- cx[11], cy[11], cost_obs, cost_lane (and beta, sigma, res_beta
-for mmd_opt) within 1e-4 relative -- unless they part at a reported
-near-tie: then the first diverging iteration is printed with the tied keys
-and the comparison stops there (S/opt/cem.py:320-333, Q1: the result is the
-last iteration's obstacle-elite 0).
+read back and compared with the oracle's trace.  Every run must reach the
+last iteration in lockstep -- identical elite sets in all 20 iterations --
+and the results must agree: cx[11], cy[11], cost_obs, cost_lane (and beta,
+sigma, res_beta for mmd_opt) within 1e-4 relative (S/opt/cem.py:320-333,
+Q1: the result is the last iteration's obstacle-elite 0).  Exceptions, each
+asserted narrowly:
+  * mmd_opt: a candidate whose beta-CEM parted from the oracle's at the one
+    near-tie that can explain it (tests/parity.py: beta_divergence) may have
+    other costs; it must not change an elite set;
+  * beta noise: rejection-sampled Beta draws may differ in ulps, which may
+    move the costs of at most B / 20 candidates per iteration (never an
+    elite set).
 """
 import numpy as np
 import pytest
 
 import oracle
 from oracle.helper import compute_obs_trajectories
-from parity import DEFAULT_COV, DEFAULT_INIT, DEFAULT_MEAN, beta_cem_trace, beta_near_tie, close, elite_equal
+from parity import DEFAULT_COV, DEFAULT_INIT, DEFAULT_MEAN, beta_cem_trace, beta_near_tie, close
 
 pytestmark = pytest.mark.gpu
 
@@ -45,8 +51,10 @@ def _per_candidate(nat, tr, cost, n):
     inner = np.ones(B, bool)
     if cost == "mmd_opt":
         res_g = nat.read("res_beta").reshape(B, 20)
-        inner &= np.all(np.abs(res_g - tr["res_beta"]) <= 1e-4 * np.abs(tr["res_beta"]) + 1e-4, axis=1)
+        inner &= np.all(np.abs(res_g - tr["res_beta"]) <= 1e-4 * np.abs(tr["res_beta"]) + 1e-6, axis=1)
         inner &= np.abs(nat.read("sigma")[:B] - tr["sigma"]) <= 1e-6 * np.abs(tr["sigma"])
+        beta_g = nat.read("beta").reshape(B, n)
+        inner &= np.all(np.abs(beta_g - tr["beta"]) <= 1e-3 * np.abs(tr["beta"]) + 1e-4, axis=1)
     return ok, inner
 
 
@@ -65,55 +73,51 @@ def test_free_run(native, cost, noise, n):
     ref = ora.solve(cost, idx, DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, xo, yo, 15.0, draws=draws, trace=trace)
     nat.begin(cost, idx, DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, xo, yo, 15.0, draws)
     assert float(np.max(trace[0]["obs"])) > float(np.min(trace[0]["obs"])), "scenario does not separate candidates"
-    diverged, inner_parted = None, set()
+    parted, moved = {}, {}
     for t in range(T):
         nat.iterate(t, 1)
         nat.sync()
         tr = trace[t]
         ok, inner = _per_candidate(nat, tr, cost, n)
         if cost == "mmd_opt" and not inner.all():
-            # a candidate's beta-CEM parted from the oracle's: only at a near-tie of its QP costs
+            # a candidate's beta-CEM parted from the oracle's: only at the near-tie that explains it
             acc, steer = nat.read("acc").reshape(B, 100), nat.read("steer").reshape(B, 100)
             st = ora.init_state(DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, draws)
             res_g = nat.read("res_beta").reshape(B, 20)
+            esum_g = nat.read("btrace").reshape(B, 20)
             for b in np.nonzero(~inner)[0]:
-                _, tie, detail = beta_near_tie(beta_cem_trace(ora, st, acc[b], steer[b], draws, t), res_g[b])
-                assert tie, f"iteration {t} candidate {b}: beta-CEM differs without a near-tie ({detail})"
-                print(f"iteration {t} candidate {b}: {detail}")
-            inner_parted.update(int(b) for b in np.nonzero(~inner)[0])
+                _, tie, detail = beta_near_tie(beta_cem_trace(ora, st, acc[b], steer[b], draws, t), res_g[b], esum_g[b])
+                assert tie, f"iteration {t} candidate {b}: beta-CEM differs without a qualifying near-tie ({detail})"
+                parted[(t, int(b))] = detail
         if not ok.all():
             bad = np.nonzero(~ok)[0]
             if cost == "mmd_opt":  # a cost moves only through its beta-CEM parting (explained above)
-                assert set(bad.tolist()) <= inner_parted, f"iteration {t}: costs of {bad} differ, beta-CEM equal"
+                assert all((t, int(b)) in parted for b in bad), f"iteration {t}: costs of {bad} differ, beta-CEM equal"
             elif noise == "beta":
                 # rejection-sampled Beta draws: ulp-level differences may move a sample's cost
                 assert bad.size <= max(1, B // 20), f"iteration {t}: {bad.size} candidates differ"
+                moved[t] = bad.tolist()
             else:
                 raise AssertionError(f"iteration {t}: candidates {bad} differ: GPU "
                                      f"{nat.read('obs_cost')[:B][bad]} oracle {tr['obs'][bad]}")
-            diverged = (t, "candidate costs", bad.tolist())
-            break
         tp = nat.read("tr_proj", np.int32).reshape(T, B)[t]
         to = nat.read("tr_obs", np.int32).reshape(T, 20)[t]
         tc = nat.read("tr_cem", np.int32).reshape(T, 5)[t]
-        same = (elite_equal(f"elite_proj[{t}]", tp, tr["perm"], tr["res_norm"], tol=1e-3)
-                and elite_equal(f"elite_obs[{t}]", to, tr["elite_obs"], tr["obs"])
-                and elite_equal(f"elite_cem[{t}]", tc, tr["elite_cem"], tr["cost20"]))
-        if not same:  # elite_equal already asserted that the difference is a near-tie
-            diverged = (t, "elite near-tie", None)
-            break
-    if diverged is not None:
-        print(f"{cost}/{noise}: runs part at iteration {diverged[0]} ({diverged[1]} {diverged[2]})")
-        assert diverged[0] >= 2, "diverged before the CEM had run two iterations"
-        return
+        # lockstep to the end: the elite sets must be identical every iteration
+        assert np.array_equal(tp, tr["perm"]), f"iteration {t}: projection order differs"
+        assert np.array_equal(to, tr["elite_obs"]), f"iteration {t}: obstacle elites {to} vs {tr['elite_obs']}"
+        assert np.array_equal(tc, tr["elite_cem"]), f"iteration {t}: cost elites {tc} vs {tr['elite_cem']}"
     got = nat.finish(trace=True)
     close("cx", got["cx"], ref[0], rtol=1e-4, atol=1e-4)
     close("cy", got["cy"], ref[1], rtol=1e-4, atol=1e-4)
-    fl = 1e-2 if cost.startswith("mmd") else 1e-5
-    close("cost_lane", got["cost_lane"], ref[2], rtol=1e-4, atol=fl)
-    close("cost_obs", got["cost_obs"], ref[3], rtol=1e-4, atol=fl)
-    if cost == "mmd_opt" and int(got["elite_obs"][T - 1][0]) not in inner_parted:
-        close("beta", got["beta"][:n], ref[4], rtol=1e-3, atol=1e-4)
-        close("sigma", got["sigma"], ref[5], rtol=1e-6, atol=0)
-        close("res_beta", got["res_beta"], ref[6], rtol=1e-4, atol=1e-4)
-    print(f"{cost}/{noise}: 20 unsynchronised iterations agree; cost_obs {float(got['cost_obs'])}")
+    e0 = int(got["elite_obs"][T - 1][0])
+    if (T - 1, e0) not in parted and e0 not in moved.get(T - 1, []):
+        fl = 1e-2 if cost.startswith("mmd") else 1e-5
+        close("cost_lane", got["cost_lane"], ref[2], rtol=1e-4, atol=fl)
+        close("cost_obs", got["cost_obs"], ref[3], rtol=1e-4, atol=fl)
+        if cost == "mmd_opt":
+            close("beta", got["beta"][:n], ref[4], rtol=1e-3, atol=1e-4)
+            close("sigma", got["sigma"], ref[5], rtol=1e-6, atol=0)
+            close("res_beta", got["res_beta"], ref[6], rtol=1e-4, atol=1e-6)
+    print(f"{cost}/{noise}: 20 iterations in lockstep; cost_obs {float(got['cost_obs'])}; "
+          f"explained beta-CEM partings {parted}; Beta-draw cost moves {moved}")

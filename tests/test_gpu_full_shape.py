@@ -45,12 +45,13 @@ def test_full_shape_iteration(native, cost, noise, n, sample):
         # beta-CEM took another path at a reported near-tie of QP costs (the
         # 2000 cost comparisons per candidate agree to ~1e-7 relative)
         res_g = nat.read("res_beta").reshape(B, 20)
+        esum_g = nat.read("btrace").reshape(B, 20)
         ok = np.abs(obs_g[idx] - obs) <= 1e-2 + 1e-4 * np.abs(obs)
         ok &= np.abs(lane_g[idx] - lane) <= 1e-2 + 1e-4 * np.abs(lane)
         for j in np.nonzero(~ok)[0]:
             b = int(idx[j])
             tr = beta_cem_trace(ora, st, acc_g[b], steer_g[b], draws, 0)
-            t0, tie, detail = beta_near_tie(tr, res_g[b])
+            t0, tie, detail = beta_near_tie(tr, res_g[b], esum_g[b])
             print(f"candidate {b}: obs GPU {obs_g[b]} oracle {obs[j]}; {detail}")
             assert tie, f"candidate {b}: obs {obs_g[b]} vs {obs[j]} not explained by a near-tie ({detail})"
         assert ok.mean() >= 0.75, f"only {ok.sum()}/{ok.size} candidates agree"

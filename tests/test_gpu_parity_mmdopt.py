@@ -108,6 +108,7 @@ def test_beta_cem_lockstep(native, n, B, H, O, variant, check, qp_iters):
         s0[:, M] = np.maximum(s0[:, M], F32(0.01))
         samples[b] = s0
     res_ref = {b: np.zeros(20, F32) for b in cand}
+    qp_rel = 0.0   # largest relative difference of a QP cost on identical inputs (sizes parity.TIE_REL)
     for tb in range(20):
         nat.run_stage(5, tb)
         bsel = nat.read("bsel", np.int32).reshape(B, 100, n)
@@ -129,6 +130,8 @@ def test_beta_cem_lockstep(native, n, B, H, O, variant, check, qp_iters):
             close(f"kred[{tb},{b}]", kred[b, s_lo:], K_red[s_lo:, lo[0], lo[1]], rtol=1e-6, atol=1e-7)
             close(f"btop[{tb},{b}]", btop[b], beta, rtol=1e-3, atol=1e-4)
             close(f"bcost[{tb},{b}]", bcost[b], cost, rtol=1e-4, atol=1e-4)
+            qp_rel = max(qp_rel, float(np.max(np.abs(bcost[b, s_lo:].astype(F64) - cost[s_lo:])
+                                              / np.maximum(np.abs(cost[s_lo:]), 1e-3))))
         nat.run_stage(7, tb)
         bel = nat.read("belite").reshape(2, B, 11, M1)[(tb + 1) & 1]
         res_beta = nat.read("res_beta").reshape(B, 20)
@@ -146,6 +149,9 @@ def test_beta_cem_lockstep(native, n, B, H, O, variant, check, qp_iters):
                 assert np.array_equal(beta_g, btop[b, imin])
                 close(f"sigma_best[{b}]", sig_g, nxt[imin, M], rtol=1e-6, atol=0)
             samples[b] = nxt
+    from parity import TIE_REL
+    print(f"n={n}: QP costs GPU vs oracle on identical inputs agree to {qp_rel:.3g} relative (TIE_REL {TIE_REL})")
+    assert qp_rel <= TIE_REL / 2, f"QP cost agreement {qp_rel:.3g} too coarse for the near-tie threshold {TIE_REL}"
     # final reduced-set MMD on the GPU's beta-CEM outputs
     nat.run_stage(8, 0)
     ctrl = nat.read("ctrl_n").reshape(B, 2, n, H)
@@ -189,16 +195,18 @@ def test_mmdopt_iteration_lockstep(native):
         close(f"res_norm[{t}]", nat.read("res_norm")[:B], tr["res_norm"], atol=1e-5)
         obs_g, lane_g = nat.read("obs_cost")[:B], nat.read("lane_cost")[:B]
         res_g = nat.read("res_beta").reshape(B, 20)
+        esum_g = nat.read("btrace").reshape(B, 20)
         beta_g, sig_g = nat.read("beta").reshape(B, n), nat.read("sigma")[:B]
         cost_ok = np.abs(obs_g - tr["obs"]) <= 1e-2 + 1e-4 * np.abs(tr["obs"])
         cost_ok &= np.abs(lane_g - tr["lane"]) <= 1e-2 + 1e-4 * np.abs(tr["lane"])
-        ok = cost_ok & np.all(np.abs(res_g - tr["res_beta"]) <= 1e-4 * np.abs(tr["res_beta"]) + 1e-4, axis=1)
+        ok = cost_ok & np.all(np.abs(res_g - tr["res_beta"]) <= 1e-4 * np.abs(tr["res_beta"]) + 1e-6, axis=1)
         ok &= np.all(np.abs(beta_g - tr["beta"]) <= 1e-3 * np.abs(tr["beta"]) + 1e-4, axis=1)
         ok &= np.abs(sig_g - tr["sigma"]) <= 1e-6 * np.abs(tr["sigma"])
         if not ok.all():
             acc, steer = nat.read("acc").reshape(B, 100), nat.read("steer").reshape(B, 100)
             for b in np.nonzero(~ok)[0]:
-                t0, tie, detail = beta_near_tie(beta_cem_trace(ora, st, acc[b], steer[b], draws, t), res_g[b])
+                t0, tie, detail = beta_near_tie(beta_cem_trace(ora, st, acc[b], steer[b], draws, t), res_g[b],
+                                                esum_g[b])
                 print(f"iteration {t} candidate {b}: obs {obs_g[b]} / {tr['obs'][b]}, sigma {sig_g[b]} / "
                       f"{tr['sigma'][b]}; {detail}")
                 assert tie, f"iteration {t} candidate {b}: beta-CEM differs without a near-tie ({detail})"
