@@ -502,10 +502,7 @@ DEVI void select_walk(Row row, Out out, int first, int last, int stride, int M, 
 //   A: A[r][h]   B: B[h][r]   C/D register i: C[h + 4 i][r]
 typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int kSampleTiles = kBzCols / 16;  // 6 tiles of 16 sample columns (89 used)
-#ifndef MPCMMD_SAMPLE_TILES
-#define MPCMMD_SAMPLE_TILES 6
-#endif
-constexpr int kTilesPerWave = MPCMMD_SAMPLE_TILES;
+constexpr int kTilesPerWave = 6;
 constexpr int kSampleWaves = kSampleTiles / kTilesPerWave;
 static_assert(kSampleTiles % kTilesPerWave == 0, "tiles per wave");
 static_assert(kTilesPerWave % 2 == 0, "sample tiles are loaded in pairs");
@@ -707,10 +704,7 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
 // From the second beta-iteration on, samples 0..10 are the previous elites:
 // their selection, kernels and QP are unchanged, k_belite carried them, and
 // only samples 11..99 are processed here.
-#ifndef MPCMMD_KER_WAVES
-#define MPCMMD_KER_WAVES 16
-#endif
-constexpr int kKerWavesMax = MPCMMD_KER_WAVES;
+constexpr int kKerWavesMax = 16;
 
 constexpr int kLptBins = 128;  // pair counts per distinct row (<= 100 samples)
 
@@ -802,14 +796,11 @@ __global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb,
   int* cnt = reinterpret_cast<int*>(smem + C.rowbuf);  // setup only
   int* fill = cnt + M;
   unsigned short* start = reinterpret_cast<unsigned short*>(fill + M);
-  double* rowsum = p.brow + size_t(b) * kBetaSamples * n;
-  const int ntri = n * (n - 1) / 2;
+  float* rowsum = p.brow + size_t(b) * kBetaSamples * n;
+  const int ntri = tri_stride(n);
   const int s_lo = first_sample(tb);
   const int i_lo = s_lo * n, i_hi = kBetaSamples * n;
   MPCMMD_STAMP(p, 16);
-#ifdef MPCMMD_WGT
-  if (tid == 0) p.wgt[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-#endif
   const int32_t* gsel = p.bsel + size_t(b) * kBetaSamples * n;
   for (int i = i_lo + tid; i < i_hi; i += blockDim.x) sl[i] = short(gsel[i]);
   for (int s = s_lo + tid; s < kBetaSamples; s += blockDim.x)
@@ -927,7 +918,6 @@ __global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb,
       const uint32_t pl = pairs[pb + c0 + min(lane, cc - 1)];
       const float cl = csg[pl >> 24];
       for (int j0 = 0; j0 < cc; j0 += 8) {
-#ifndef MPCMMD_KER_NOSUM
         float v[8];
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
@@ -949,21 +939,16 @@ __global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb,
           }
         }
         const float sum = transpose_sum8(v);
-#endif
         // lane group j = lane >> 3 takes pair j0 + j
         const int jg = j0 + (lane >> 3);
         const bool live = jg < cc;
         const uint32_t pkj = __shfl(pl, jg, 64);
         const float cj = __shfl(cl, jg, 64);
         const int s = pkj >> 24, k = live ? int(pkj >> 18) & 63 : 0;
-#ifndef MPCMMD_KER_NOSUM
-        if ((lane & 7) == 4 && live) rowsum[s * n + k] = double(sum);
-#endif
-#ifndef MPCMMD_KER_NOGATHER
+        if ((lane & 7) == 4 && live) rowsum[s * n + k] = sum;
         const short* sls = sl + s * n;
         float* kr = kbase + (pkj & 0x3FFFFu);
         for (int kk = lane & 7; kk < k; kk += 8) kr[kk] = __builtin_amdgcn_exp2f(rb[sls[kk]] * cj);
-#endif
       }
     }
     wave_sync();  // the gathers read the copy before the next row overwrites it
@@ -993,17 +978,15 @@ __global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb,
     }
   }
   MPCMMD_STAMP(p, 20);
-#ifdef MPCMMD_WGT
-  __syncthreads();
-  if (tid == 0) p.wgt[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
 }
 
 // ------------------------------------------------------------------------
 // k_bqp: compute_beta_reduced (compute_beta.py:70-91) for every sample:
 // C = K_red + 0.05 I, C x1 = g, C x2 = 1, beta = x1 + ((1 - sum x1) / sum x2) x2
-// (the (n+1) KKT system), cost = beta^T K beta - 2 g^T beta with
-// beta^T C beta = |L^T beta|^2.  All in fp64.
+// (the (n+1) KKT system).  The factorisation and the solves are fp32, the
+// reference's precision (jnp.linalg.solve on fp32, compute_beta.py:79); the
+// cost beta^T K beta - 2 g^T beta is accumulated in fp64 from the fp32 beta
+// and the re-read K_red, so it carries no factorisation error.
 //
 // A quad (4 lanes) per QP, 16 QPs per wave: lane q owns rows i = 4t + q of
 // the (padded to NP) matrix, in registers.  Right-looking Cholesky; the
@@ -1014,6 +997,15 @@ __global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb,
 // identity with zero right-hand sides.
 // value of quad lane l (0..3) in every lane of the quad; l is a constant
 // after unrolling, so the switch folds
+DEVI float quad_bcast(float v, int l) {
+  const int b = __float_as_int(v);
+  switch (l & 3) {
+    case 0: return __int_as_float(dpp_i<0x00>(b));
+    case 1: return __int_as_float(dpp_i<0x55>(b));
+    case 2: return __int_as_float(dpp_i<0xAA>(b));
+    default: return __int_as_float(dpp_i<0xFF>(b));
+  }
+}
 DEVI double quad_bcast(double v, int l) {
   switch (l & 3) {
     case 0: return dpp_d<0x00>(v);
@@ -1023,13 +1015,26 @@ DEVI double quad_bcast(double v, int l) {
   }
 }
 // sum over the quad, bit-identical in its 4 lanes
+DEVI float quad_sum(float v) {
+  v = v + __int_as_float(dpp_i<0xB1>(__float_as_int(v)));  // quad_perm(1,0,3,2)
+  return v + __int_as_float(dpp_i<0x4E>(__float_as_int(v)));  // quad_perm(2,3,0,1)
+}
 DEVI double quad_sum(double v) {
-  v = v + dpp_d<0xB1>(v);  // quad_perm(1,0,3,2)
-  return v + dpp_d<0x4E>(v);  // quad_perm(2,3,0,1)
+  v = v + dpp_d<0xB1>(v);
+  return v + dpp_d<0x4E>(v);
+}
+// 1 / sqrt(x): v_rsq_f32 and one Newton step
+DEVI float rsqrt_nr(float x) {
+  const float y = __builtin_amdgcn_rsqf(x);
+  return y * fmaf(-0.5f * x, y * y, 1.5f);
 }
 
+// K_red of the workgroup's QPs is staged in LDS first (consecutive
+// threads copy consecutive entries of one QP's triangle: coalesced), so the
+// per-lane row gathers of the factorisation and the cost read LDS, not
+// scattered global lines.
 template <int NP>
-DEVI void bqp_quad(const Params& p, int tb) {
+DEVI void bqp_quad(const Params& p, int tb, float* kl) {
   constexpr int T4 = NP / 4;
   const int n = p.n, M = p.M, q = threadIdx.x & 3;
   const int s_lo = first_sample(tb), per = kBetaSamples - s_lo;
@@ -1037,176 +1042,207 @@ DEVI void bqp_quad(const Params& p, int tb) {
   const bool ok = gq < p.nb * per;
   const int gqc = ok ? gq : 0;
   const int b = p.b0 + gqc / per, s = s_lo + gqc % per;
-  const int ntri = n * (n - 1) / 2;
-  const float* kr = p.bkred + (size_t(b) * kBetaSamples + s) * ntri;
-  const double* br = p.brow + (size_t(b) * kBetaSamples + s) * n;
-  const double inv_m = double(1.0f / float(M));
-  const double cdiag = double(1.0f + 0.05f);
-  const double delta = cdiag - 1.0;  // C_ii - K_ii (K_ii = exp(0) = 1)
-  // own rows: A[t][k] = C[4t+q][k], k <= 4t+3 (k > row: 0)
-  double A[T4][NP];
-  double a1[T4], a2[T4], rin[T4];
-  // every load unconditional (clamped address, value masked afterwards) so
-  // they are all in flight together: one memory latency, not one per entry
-  float kv[T4][NP];
-  double bv[T4];
+  const int ntri = tri_stride(n);
+  {  // wave w copies the rows of QPs w, w + W, ... as float4s, four rows in flight
+    const int nq = blockDim.x >> 2, q0 = blockIdx.x * nq, total = p.nb * per, n4 = ntri >> 2;
+    const int lane = threadIdx.x & 63, W = blockDim.x >> 6;
+    float4* kl4 = reinterpret_cast<float4*>(kl);
+    for (int c0 = 0; c0 < n4; c0 += 64) {
+      const int c = min(c0 + lane, n4 - 1);
+      for (int j0 = 0; j0 < nq; j0 += W * 4) {
+        float4 v[4];
 #pragma unroll
-  for (int t = 0; t < T4; ++t) {
-    const int i = 4 * t + q;
-    const int ic = min(i, n - 1);
+        for (int u = 0; u < 4; ++u) {
+          const int j = j0 + (threadIdx.x >> 6) + W * u, g = min(q0 + min(j, nq - 1), total - 1);
+          const float4* src = reinterpret_cast<const float4*>(
+              p.bkred + (size_t(p.b0 + g / per) * kBetaSamples + s_lo + g % per) * ntri);
+          v[u] = src[c];
+        }
 #pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      if (k > 4 * t + 3) continue;
-      const int e = ic > 0 ? ic * (ic - 1) / 2 + max(min(k, ic - 1), 0) : 0;  // always a valid entry (n >= 2)
-      kv[t][k] = kr[e];
+        for (int u = 0; u < 4; ++u) {
+          const int j = j0 + (threadIdx.x >> 6) + W * u;
+          if (j < nq && c0 + lane < n4) kl4[j * n4 + c] = v[u];
+        }
+      }
     }
-    bv[t] = br[ic];
+    __syncthreads();
   }
+  const float* kr = kl + (threadIdx.x >> 2) * ntri;
+  const float* br = p.brow + (size_t(b) * kBetaSamples + s) * n;
+  const double inv_m = double(1.0f / float(M));
+  const float cdiag = 1.0f + 0.05f;
+  // entry (i, k < i) of K_red (k_bkernel's strict lower triangle); always a
+  // valid address (clamped), the value masked by the caller
+  auto kidx = [&](int i, int k) {
+    const int ic = min(i, n - 1);
+    return ic > 0 ? ic * (ic - 1) / 2 + max(min(k, ic - 1), 0) : 0;
+  };
+  // own rows: A[t][k] = C[4t+q][k], k <= 4t+3; loaded as K_red (every load
+  // unconditional, so they are all in flight together), factored in place
+  float A[T4][NP];
+  float a1[T4], a2[T4], rin[T4];
 #pragma unroll
   for (int t = 0; t < T4; ++t) {
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+      if (k <= 4 * t + 3) A[t][k] = kr[kidx(4 * t + q, k)];
     const int i = 4 * t + q;
-    a1[t] = i < n ? bv[t] * inv_m : 0.0;  // g
-    a2[t] = i < n ? 1.0 : 0.0;
-    rin[t] = 0.0;
+    const float g = float(double(br[min(i, n - 1)]) * inv_m);
+    a1[t] = i < n ? g : 0.0f;
+    a2[t] = i < n ? 1.0f : 0.0f;
+    rin[t] = 0.0f;
   }
-  // Cholesky, left-looking by columns: column k of C (still fp32 in kv)
-  // minus sum_{j<k} L_ij L_kj, in the order j = 0, 1, ... (the right-looking
-  // update order, so the same roundings), then scaled.  The fp32 input of
-  // columns > k and the fp64 factor of columns < k are live together, never
-  // both in full, which keeps the kernel at two waves per SIMD.
+  // C in place: strict lower part from K_red, the diagonal 1.05 (1 for the
+  // padding rows), entries above the diagonal 0
+#pragma unroll
+  for (int t = 0; t < T4; ++t)
+#pragma unroll
+    for (int k = 0; k <= 4 * t + 3; ++k) {
+      const int i = 4 * t + q;
+      float v = (k < i && i < n) ? A[t][k] : 0.0f;
+      if (k == i) v = i < n ? cdiag : 1.0f;
+      A[t][k] = v;
+    }
+  // Cholesky, right-looking: column k scaled by 1 / sqrt(C_kk), then the
+  // trailing columns c > k updated (every update of a step independent)
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
     const int tk = k >> 2, qk = k & 3;
-    double sc[T4];
-#pragma unroll
-    for (int t = tk; t < T4; ++t) {
-      const int i = 4 * t + q;
-      double v = (k < i && i < n) ? double(kv[t][k]) : 0.0;
-      if (k == i) v = i < n ? cdiag : 1.0;
-      sc[t] = v;
-    }
-#pragma unroll
-    for (int j = 0; j < k; ++j) {
-      const double lkj = quad_bcast(A[tk][j], qk);  // L_kj from the lane owning row k
-#pragma unroll
-      for (int t = tk; t < T4; ++t) sc[t] = fma(-A[t][j], lkj, sc[t]);
-    }
-    const double sv = sc[tk];
-    double y = __builtin_amdgcn_rsq(sv);  // 1/sqrt: v_rsq_f64 + two Newton steps
-    y = y * fma(-0.5 * sv, y * y, 1.5);
-    y = y * fma(-0.5 * sv, y * y, 1.5);
-    const double ry = quad_bcast(y, qk);
-    const double dk = sv * y;
+    const float sv = quad_bcast(A[tk][k], qk);  // the pivot, from the lane owning row k
+    const float y = rsqrt_nr(sv);
     if (q == qk) rin[tk] = y;
 #pragma unroll
     for (int t = tk; t < T4; ++t) {
-      const double v = sc[t] * ry;
-      A[t][k] = t > tk ? v : (q > qk ? v : (q == qk ? dk : 0.0));
+      const float v = A[t][k] * y;
+      A[t][k] = t > tk ? v : (q > qk ? v : (q == qk ? sv * y : 0.0f));
+    }
+#pragma unroll
+    for (int c = k + 1; c < NP; ++c) {
+      const int tc = c >> 2;
+      const float lck = quad_bcast(A[tc][k], c & 3);  // L_ck from the lane owning row c
+#pragma unroll
+      for (int t = tc; t < T4; ++t) A[t][c] = fmaf(-A[t][k], lck, A[t][c]);
     }
   }
   // forward: L y = (g, 1)
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
     const int tj = j >> 2, qj = j & 3;
-    const double y1 = a1[tj] * rin[tj], y2 = a2[tj] * rin[tj];
+    const float y1 = a1[tj] * rin[tj], y2 = a2[tj] * rin[tj];
     if (q == qj) {
       a1[tj] = y1;
       a2[tj] = y2;
     }
-    const double b1 = quad_bcast(y1, qj), b2 = quad_bcast(y2, qj);
+    const float b1 = quad_bcast(y1, qj), b2 = quad_bcast(y2, qj);
 #pragma unroll
     for (int t = tj; t < T4; ++t) {
-      const double lij = (t == tj && q <= qj) ? 0.0 : A[t][j];
-      a1[t] = fma(-lij, b1, a1[t]);
-      a2[t] = fma(-lij, b2, a2[t]);
+      const float lij = (t == tj && q <= qj) ? 0.0f : A[t][j];
+      a1[t] = fmaf(-lij, b1, a1[t]);
+      a2[t] = fmaf(-lij, b2, a2[t]);
     }
   }
   // C^-1 = L^-T L^-1, so with y1 = L^-1 g, y2 = L^-1 1: sum x1 = y2 . y1,
   // sum x2 = |y2|^2 and beta = L^-T (y1 + alpha y2) -- one backward sweep
-  double s1 = 0.0, s2 = 0.0;
+  float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll
   for (int t = 0; t < T4; ++t) {  // padding rows hold y = 0
-    s1 = fma(a2[t], a1[t], s1);
-    s2 = fma(a2[t], a2[t], s2);
+    s1 = fmaf(a2[t], a1[t], s1);
+    s2 = fmaf(a2[t], a2[t], s2);
   }
   s1 = quad_sum(s1);
   s2 = quad_sum(s2);
-  const double alpha = (1.0 - s1) / s2;
+  const float alpha = (1.0f - s1) / s2;
 #pragma unroll
-  for (int t = 0; t < T4; ++t) a1[t] = fma(alpha, a2[t], a1[t]);
+  for (int t = 0; t < T4; ++t) a1[t] = fmaf(alpha, a2[t], a1[t]);
   // backward: L^T beta = y1 + alpha y2 (beta overwrites it row by row, last row first)
 #pragma unroll
   for (int j = NP - 1; j >= 0; --j) {
     const int tj = j >> 2, qj = j & 3;
-    double p1 = 0.0;
+    float p1 = 0.0f;
 #pragma unroll
     for (int t = tj; t < T4; ++t) {
-      const double lij = (t == tj && q <= qj) ? 0.0 : A[t][j];
-      p1 = fma(lij, a1[t], p1);
+      const float lij = (t == tj && q <= qj) ? 0.0f : A[t][j];
+      p1 = fmaf(lij, a1[t], p1);
     }
     p1 = quad_sum(p1);
     if (q == qj) a1[tj] = (a1[tj] - p1) * rin[tj];
   }
   float bf[T4];
-  double bd[T4];
+#pragma unroll
+  for (int t = 0; t < T4; ++t) bf[t] = 4 * t + q < n ? a1[t] : 0.0f;
+  // cost = beta^T K beta - 2 g^T beta in fp64, K = K_red re-read (unit
+  // diagonal): r_i = sum_{k<i} K_ik beta_k by columns k, column k + 1's
+  // entries in flight while column k is summed (two columns live, not the
+  // whole triangle); row i contributes beta_i (beta_i + 2 r_i)
+  double r[T4];
+  float kc[T4], kn[T4];
 #pragma unroll
   for (int t = 0; t < T4; ++t) {
-    bf[t] = 4 * t + q < n ? float(a1[t]) : 0.0f;
-    bd[t] = double(bf[t]);
+    r[t] = 0.0;
+    kc[t] = kr[kidx(4 * t + q, 0)];
   }
-  // cost = |L^T beta|^2 - delta |beta|^2 - 2 g^T beta
-  double c1 = 0.0;
 #pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    const int ti = i >> 2, qi = i & 3;
-    double pi = 0.0;
+  for (int k = 0; k < NP; ++k) {
 #pragma unroll
-    for (int t = ti; t < T4; ++t) {
-      const double lki = (t == ti && q < qi) ? 0.0 : A[t][i];
-      pi = fma(lki, bd[t], pi);
+    for (int t = (k + 1) >> 2; t < T4; ++t) kn[t] = kr[kidx(4 * t + q, min(k + 1, NP - 1))];
+    __builtin_amdgcn_sched_barrier(0);
+    const double bk = double(quad_bcast(bf[k >> 2], k & 3));
+#pragma unroll
+    for (int t = k >> 2; t < T4; ++t) {
+      const int i = 4 * t + q;
+      r[t] = (k < i && i < n) ? fma(double(kc[t]), bk, r[t]) : r[t];
+      kc[t] = kn[t];
     }
-    pi = quad_sum(pi);
-    c1 = fma(pi, pi, c1);
+    __builtin_amdgcn_sched_barrier(0);
   }
-  double c2 = 0.0, c3 = 0.0;
+  double c1 = 0.0, c3 = 0.0;
 #pragma unroll
   for (int t = 0; t < T4; ++t) {
-    c2 = fma(bd[t], bd[t], c2);
-    // g again (re-read, not kept in registers through the factorisation)
     const int i = 4 * t + q;
-    const double gt = i < n ? br[min(i, n - 1)] * inv_m : 0.0;
-    c3 = fma(gt, bd[t], c3);
+    const double bi = double(bf[t]);
+    c1 = fma(bi, fma(2.0, r[t], bi), c1);
+    c3 = fma(i < n ? double(br[min(i, n - 1)]) * inv_m : 0.0, bi, c3);
   }
-  c2 = quad_sum(c2);
+  c1 = quad_sum(c1);
   c3 = quad_sum(c3);
   if (!ok) return;
   float* bt = p.btop + (size_t(b) * kBetaSamples + s) * n;
 #pragma unroll
   for (int t = 0; t < T4; ++t)
     if (4 * t + q < n) bt[4 * t + q] = bf[t];
-  if (q == 0) p.bcost[size_t(b) * kBetaSamples + s] = float((c1 - delta * c2) - 2.0 * c3);
+  if (q == 0) p.bcost[size_t(b) * kBetaSamples + s] = float(c1 - 2.0 * c3);
 }
 
 HDI int qp_np(int n) { return n <= 8 ? 8 : (n <= 16 ? 16 : (n <= 24 ? 24 : (n <= 32 ? 32 : (n <= 48 ? 48 : 64)))); }
-constexpr int kQpThreads = 256;  // 64 QPs per workgroup
+constexpr int kQpThreads = 128;  // 32 QPs per workgroup (their K_red in LDS: 30 KB at n = 22)
 
-#ifndef MPCMMD_QP24_OCC
-#define MPCMMD_QP24_OCC 2
-#endif
 template <int NP>
-__global__ __launch_bounds__(kQpThreads, NP == 24 ? MPCMMD_QP24_OCC : (NP == 16 ? 3 : 1)) void k_bqp(Params p, int tb) {
-  bqp_quad<NP>(p, tb);
+__global__ __launch_bounds__(kQpThreads, NP == 24 ? 3 : (NP <= 16 ? 4 : 2)) void k_bqp(Params p, int tb) {
+  extern __shared__ __attribute__((aligned(16))) float kl[];
+  bqp_quad<NP>(p, tb, kl);
 }
 
 // k_bqp_wave: the same QP for 32 < n <= 64, one wave per QP, lane i owns
-// row i of C (NP doubles in registers).  Right-looking Cholesky with the
+// row i of C (NP floats in registers).  Right-looking Cholesky with the
 // column entries broadcast by v_readlane (entries above the diagonal are
 // left stale and zeroed when their column is reached, never read); forward
 // solves for g and 1 together; then, since C^-1 = L^-T L^-1,
 //   sum x1 = y2.y1, sum x2 = |y2|^2, beta = L^-T (y1 + alpha y2),
-// one backward solve (column sums as wave reductions).  The cost is
-// beta^T K beta - 2 g^T beta on the fp32-rounded beta with K_red re-read
-// (same value as the quad kernel's |L^T beta|^2 - delta |beta|^2 form).
+// one backward solve (column sums as wave reductions).  fp32 like the quad
+// kernel; the cost beta^T K beta - 2 g^T beta in fp64 on the fp32 beta with
+// K_red re-read.
+DEVI float readlane_f(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+DEVI float wave_total(float v) {
+  int b = __float_as_int(v);
+  v += __int_as_float(dpp_i<0xB1>(b));
+  v += __int_as_float(dpp_i<0x4E>(__float_as_int(v)));
+  v += __int_as_float(dpp_i<0x124>(__float_as_int(v)));
+  v += __int_as_float(dpp_i<0x128>(__float_as_int(v)));
+  v += __int_as_float(dpp_i<0x142, 0xA>(__float_as_int(v)));
+  v += __int_as_float(dpp_i<0x143, 0xC>(__float_as_int(v)));
+  return readlane_f(v, 63);
+}
+
 template <int NP>
 __global__ __launch_bounds__(256) void k_bqp_wave(Params p, int tb) {
   const int lane = threadIdx.x & 63;
@@ -1215,72 +1251,69 @@ __global__ __launch_bounds__(256) void k_bqp_wave(Params p, int tb) {
   const int gq = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (gq >= p.nb * per) return;  // whole waves
   const int b = p.b0 + gq / per, s = s_lo + gq % per;
-  const int ntri = n * (n - 1) / 2;
+  const int ntri = tri_stride(n);
   const float* kr = p.bkred + (size_t(b) * kBetaSamples + s) * ntri;
-  const double* br = p.brow + (size_t(b) * kBetaSamples + s) * n;
+  const float* br = p.brow + (size_t(b) * kBetaSamples + s) * n;
   const double inv_m = double(1.0f / float(M));
-  const double cdiag = double(1.0f + 0.05f);
+  const float cdiag = 1.0f + 0.05f;
   const bool real = lane < n;
-  double A[NP];
+  float A[NP];
   const int ic = min(lane, n - 1);
 #pragma unroll
   for (int k = 0; k < NP; ++k) {  // unconditional loads (clamped entry), masked after
     const int e = ic > 0 ? ic * (ic - 1) / 2 + max(min(k, ic - 1), 0) : 0;
-    A[k] = double(kr[e]);
+    A[k] = kr[e];
   }
-  const double brv = br[ic];
+  const double gd = real ? double(br[ic]) * inv_m : 0.0;
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
-    double v = (k < lane && real) ? A[k] : 0.0;
-    if (k == lane) v = real ? cdiag : 1.0;
+    float v = (k < lane && real) ? A[k] : 0.0f;
+    if (k == lane) v = real ? cdiag : 1.0f;
     A[k] = v;
   }
-  const double g = real ? brv * inv_m : 0.0;
-  double rdiag = 1.0;
+  float rdiag = 1.0f;
   // Cholesky, column j
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
-    const double djj = readlane_d(A[j], j);
-    double y = __builtin_amdgcn_rsq(djj);  // 1/sqrt: v_rsq_f64 + two Newton steps
-    y = y * fma(-0.5 * djj, y * y, 1.5);
-    y = y * fma(-0.5 * djj, y * y, 1.5);
-    const double lij = A[j] * y;
-    A[j] = lane > j ? lij : (lane == j ? djj * y : 0.0);
+    const float djj = readlane_f(A[j], j);
+    const float y = rsqrt_nr(djj);
+    const float lij = A[j] * y;
+    A[j] = lane > j ? lij : (lane == j ? djj * y : 0.0f);
     if (lane == j) rdiag = y;
 #pragma unroll
-    for (int k = j + 1; k < NP; ++k) A[k] = fma(-A[j], readlane_d(A[j], k), A[k]);
+    for (int k = j + 1; k < NP; ++k) A[k] = fmaf(-A[j], readlane_f(A[j], k), A[k]);
   }
   // forward: L y = (g, 1)
-  double y1 = g, y2 = real ? 1.0 : 0.0;
+  float y1 = float(gd), y2 = real ? 1.0f : 0.0f;
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
-    const double t1 = readlane_d(y1 * rdiag, j), t2 = readlane_d(y2 * rdiag, j);
-    y1 = lane == j ? t1 : fma(-A[j], t1, y1);
-    y2 = lane == j ? t2 : fma(-A[j], t2, y2);
+    const float t1 = readlane_f(y1 * rdiag, j), t2 = readlane_f(y2 * rdiag, j);
+    y1 = lane == j ? t1 : fmaf(-A[j], t1, y1);
+    y2 = lane == j ? t2 : fmaf(-A[j], t2, y2);
   }
-  const double s1 = wave_total(y2 * y1), s2 = wave_total(y2 * y2);
-  const double alpha = (1.0 - s1) / s2;
-  const double wv = fma(alpha, y2, y1);
+  const float s1 = wave_total(y2 * y1), s2 = wave_total(y2 * y2);
+  const float alpha = (1.0f - s1) / s2;
+  const float wv = fmaf(alpha, y2, y1);
   // backward: L^T beta = w
-  double bet = 0.0;
+  float bet = 0.0f;
 #pragma unroll
   for (int j = NP - 1; j >= 0; --j) {
-    const double r = wave_total(A[j] * bet);
+    const float r = wave_total(A[j] * bet);
     if (lane == j) bet = (wv - r) * rdiag;
   }
-  const float bf = real ? float(bet) : 0.0f;
+  const float bf = real ? bet : 0.0f;
   const double bd = double(bf);
   // cost = bd^T K bd - 2 g^T bd, K = K_red (unit diagonal)
   double kb = bd;
 #pragma unroll 8
   for (int k = 0; k < NP; ++k) {
-    const double bk = readlane_d(bd, k);
+    const double bk = double(readlane_f(bf, k));
     if (k != lane && real && k < n) {
       const int e = k < lane ? lane * (lane - 1) / 2 + k : k * (k - 1) / 2 + lane;
       kb = fma(double(kr[e]), bk, kb);
     }
   }
-  const double c1 = wave_total(bd * kb), c3 = wave_total(g * bd);
+  const double c1 = wave_total(bd * kb), c3 = wave_total(gd * bd);
   float* bt = p.btop + (size_t(b) * kBetaSamples + s) * n;
   if (real) bt[lane] = bf;
   if (lane == 0) p.bcost[size_t(b) * kBetaSamples + s] = float(c1 - 2.0 * c3);
@@ -1294,15 +1327,17 @@ __global__ __launch_bounds__(256) void k_bqp_wave(Params p, int tb) {
 // the block sums of u u^T are row-of-16 DPP reductions.  LDS holds only the
 // block sums (nblk x 66 fp64) and small bookkeeping.
 struct EliteLds {
-  size_t Gb, misc, carry, total;
+  size_t Gb, misc, carry, ublk, total;
 };
+constexpr int kUPitch = 12;  // doubles per position row of the per-wave u staging
 HDI EliteLds elite_lds(int M1) {
   EliteLds L{};
   const int nblk = (M1 + 15) / 16;
   L.Gb = 0;
   L.misc = (size_t(nblk) * 66 * 8 + 15) & ~size_t(15);
   L.carry = L.misc + 1024;
-  L.total = L.carry + size_t(kBetaElite) * (2 * kMaxReduced + 2) * 4;
+  L.ublk = (L.carry + size_t(kBetaElite) * (2 * kMaxReduced + 2) * 4 + 15) & ~size_t(15);
+  L.total = L.ublk + size_t(kThreads / 64) * 16 * kUPitch * 8;  // one 16-position block per wave
   return L;
 }
 
@@ -1426,15 +1461,36 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
         p.genm[size_t(b) * pos_pad(M) + j] = double(float(m));
       }
     }
-    // level 1: block sums of u u^T over 16 positions (66 packed entries)
-    const int blk = j >> 4;
+    // level 1: block sums G = U^T U of u u^T over each 16-position block (66
+    // packed entries) on fp64 MFMA: the wave's four blocks one at a time, the
+    // block's u rows staged in the wave's LDS slice, then 4 x
+    // v_mfma_f64_16x16x4 with A = B = U (lane (r, h) of step s: feature r of
+    // position 4 s + h; features 11..15 zero)
+    double* ub = reinterpret_cast<double*>(smem + C.ublk) + (tid >> 6) * 16 * kUPitch;
+    const int lane = tid & 63, r = lane & 15, h = lane >> 4;
 #pragma unroll
-    for (int a = 0; a < 11; ++a)
+    for (int k = 0; k < 4; ++k) {
+      const int blk = (j >> 6) * 4 + k;  // wave-uniform
+      if ((lane >> 4) == k) {
 #pragma unroll
-      for (int c = a; c < 11; ++c) {
-        const double t = row16_sum(u[a] * u[c]);
-        if ((j & 15) == 0 && blk < nblk) Gb[blk * 66 + sym11(a, c)] = t;
+        for (int q = 0; q < kBetaElite; ++q) ub[(lane & 15) * kUPitch + q] = u[q];
+        ub[(lane & 15) * kUPitch + 11] = 0.0;
       }
+      wave_sync();
+      d4 G = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const double x = r < 11 ? ub[(4 * st + h) * kUPitch + r] : 0.0;
+        G = mfma64(x, x, G);
+      }
+      wave_sync();
+      // register i: G[h + 4 i][r]; the packed upper triangle a <= c
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int a = h + 4 * i;
+        if (blk < nblk && a <= r && r < 11) Gb[blk * 66 + sym11(a, r)] = G[i];
+      }
+    }
   }
   __syncthreads();
   // block prefix: phib[blk] <- Phi at the start of blk = I + sum_{<blk} / d
@@ -1715,14 +1771,7 @@ void launch_bsample(const Params& p, int tb, hipStream_t s) {
 // waves per candidate: ~16 single-wave workgroups per SIMD over the launch,
 // at most 16 per candidate (B = 1024: 8 -> 16 measured -8.5%; the 512-candidate
 // groups of the two-stream split: 25 -> 16 +1%)
-int sel_waves(int nb) {
-  static const int env = [] {
-    const char* e = std::getenv("MPCMMD_SEL_WAVES");  // experiments: waves per candidate
-    return e ? std::atoi(e) : 0;
-  }();
-  if (env > 0) return env;
-  return std::max(4, std::min(16, 16384 / std::max(1, nb)));
-}
+int sel_waves(int nb) { return std::max(4, std::min(16, 16384 / std::max(1, nb))); }
 
 template <int NQ>
 void launch_bselect_q(const Params& p, int tb, hipStream_t s) {
@@ -1765,18 +1814,19 @@ void launch_bqp(const Params& p, int tb, hipStream_t s) {
   const int qps = p.nb * (kBetaSamples - first_sample(tb));
   const dim3 grid((qps * 4 + kQpThreads - 1) / kQpThreads);
   const dim3 grid_wave((qps + 3) / 4);
+  const size_t lds = size_t(kQpThreads / 4) * tri_stride(p.n) * 4;
   switch (qp_np(p.n)) {
     case 8:
-      hipLaunchKernelGGL((k_bqp<8>), grid, dim3(kQpThreads), 0, s, p, tb);
+      hipLaunchKernelGGL((k_bqp<8>), grid, dim3(kQpThreads), lds, s, p, tb);
       return;
     case 16:
-      hipLaunchKernelGGL((k_bqp<16>), grid, dim3(kQpThreads), 0, s, p, tb);
+      hipLaunchKernelGGL((k_bqp<16>), grid, dim3(kQpThreads), lds, s, p, tb);
       return;
     case 24:
-      hipLaunchKernelGGL((k_bqp<24>), grid, dim3(kQpThreads), 0, s, p, tb);
+      hipLaunchKernelGGL((k_bqp<24>), grid, dim3(kQpThreads), lds, s, p, tb);
       return;
     case 32:
-      hipLaunchKernelGGL((k_bqp<32>), grid, dim3(kQpThreads), 0, s, p, tb);
+      hipLaunchKernelGGL((k_bqp<32>), grid, dim3(kQpThreads), lds, s, p, tb);
       return;
     case 48:
       hipLaunchKernelGGL((k_bqp_wave<48>), grid_wave, dim3(256), 0, s, p, tb);
@@ -1790,11 +1840,7 @@ void launch_bqp(const Params& p, int tb, hipStream_t s) {
 template <int NV4>
 void launch_bkernel_v(const Params& p, int tb, int wv, int split, hipStream_t s) {
   const KerLds k = ker_lds(p.M, p.n, wv);
-  static const int lpt = [] {
-    const char* e = std::getenv("MPCMMD_KER_NOLPT");  // experiments: row-index grab order
-    return e && std::atoi(e) > 0 ? 0 : 1;
-  }();
-  hipLaunchKernelGGL((k_bkernel<NV4>), dim3(p.nb * split), dim3(64 * wv), k.total, s, p, tb, split, lpt);
+  hipLaunchKernelGGL((k_bkernel<NV4>), dim3(p.nb * split), dim3(64 * wv), k.total, s, p, tb, split, 1);
 }
 
 void launch_bkernel(const Params& p, int tb, hipStream_t s) {
@@ -1802,11 +1848,6 @@ void launch_bkernel(const Params& p, int tb, hipStream_t s) {
   // parts per candidate: enough workgroups to fill the chip
   int split = 1;
   while (split < 8 && p.nb * split < 512) split <<= 1;
-  static const int split_env = [] {
-    const char* e = std::getenv("MPCMMD_KER_SPLIT");  // experiments: parts per candidate
-    return e ? std::atoi(e) : 0;
-  }();
-  if (split_env > 0) split = split_env;
   switch (dist_stride(p.M) >> 8) {
 #define MPCMMD_KER_CASE(V) \
   case V:                  \

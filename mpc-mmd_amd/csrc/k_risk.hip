@@ -89,25 +89,40 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
   }
   __syncthreads();
   const float* bpl = p.noise == 1 ? p.bplane + size_t(b) * 2 * H * S : nullptr;
+  const size_t HS = size_t(H) * S;
   for (int r = threadIdx.x; r < S; r += blockDim.x) {
     float x = cf.st0[0], y = cf.st0[1], vx = cf.st0[2], vy = cf.st0[3], psi = cf.st0[4];
     float cb = 0.0f, lb = 0.0f, ub = 0.0f;
     bool nan = false;
+    // the step's three noise values (gaussian: acc / steer / const normals,
+    // beta: the two Beta draws and the const normal), the next step's loads
+    // issued one step ahead so the scan does not wait on L2 every step
+    const float* rl = cf.roll + size_t(t) * 3 * HS + r;
+    const float* n01 = p.noise == 1 ? bpl + r : rl;  // [2][H][S] planes or roll rows 0, 1
+    float c0 = n01[0], c1 = n01[HS], c2 = rl[2 * HS];
     for (int h = 0; h < H; ++h) {
       // residual of the recorded state (x_roll[:, h] = state before step h)
       for (int o = 0; o < O; ++o) {
-        const float c = f_bar(x, y, L.xo[o * H + h], L.yo[o * H + h]);
-        nan |= (c != c);
-        cb = fmaxf(cb, c);
+        // |x - x_o| >= a gives (x - x_o)^2 / a^2 >= 1 (monotone roundings), so
+        // f_bar <= 0 cannot raise the maximum: skipped (whole waves, as a rule)
+        const float xo = L.xo[o * H + h];
+        if (!(fabsf(x - xo) >= kObsA)) {
+          const float c = f_bar(x, y, xo, L.yo[o * H + h]);
+          nan |= (c != c);
+          cb = fmaxf(cb, c);
+        }
       }
       const float l1 = -y + p.y_lb, u1 = y - p.y_ub;
-      nan |= (y != y);
+      nan |= (y != y) | (x != x);
       lb = fmaxf(lb, l1);
       ub = fmaxf(ub, u1);
       if (h == H - 1) break;  // the last step's state is never recorded
+      const size_t hn = size_t(h + 1) * S;
+      const float f0 = n01[hn], f1 = n01[HS + hn], f2 = rl[2 * HS + hn];
       float an, sn;
-      noisy_control<true>(p, cf, t, r, h, L.a[h], L.st[h], an, sn, bpl);
+      noisy_from(p, L.a[h], L.st[h], c0, c1, c2, an, sn);
       bicycle_step(x, y, vx, vy, psi, an, sn);
+      c0 = f0, c1 = f1, c2 = f2;
     }
     const float qnan = __int_as_float(0x7fc00000);
     L.cbar[r] = nan ? qnan : cb;
@@ -159,39 +174,72 @@ __global__ __launch_bounds__(256) void k_gamma_tab(Params p, int t) {
   o[3 * size_t(plane)] = squeeze ? g.lw : -g.lw;
 }
 
-// Beta draws of every (candidate, row, step) of the baseline rollouts:
-// thread (r) of block (h, b); written [B][2][H][S] for k_risk_baseline, so
-// the rollout kernel stays fp32 and its occupancy is not set by the fp64
-// gamma sampler
+// Beta draws of every (candidate, row, step) of the baseline rollouts,
+// written [B][2][H][S] for k_risk_baseline (the rollout kernel stays fp32 and
+// its occupancy is not set by the fp64 gamma sampler).  The attempt table
+// depends only on (row r, step h) (Q2): a workgroup stages attempt 0 of the
+// four gammas for 64 rows of one step in LDS once and applies it to
+// kBetaCands candidates of one configuration (wave w takes candidates w, w +
+// 4, ...; lane = row), so the table is read from L2 once per 16 candidates
+// instead of once per candidate.  The rarely needed attempts 1-3 come from
+// the table in global memory; more than that goes to k_beta_fix.
+constexpr int kBetaCands = 16;
+constexpr int kBetaRows = 64;
+
 __global__ __launch_bounds__(256) void k_beta_planes(Params p, int t) {
   const int S = p.S, H = p.H;
-  const int r = blockIdx.x * blockDim.x + threadIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const double* gtab = p.gtab + size_t(b / p.B) * gtab_stride(S, H);  // this candidate's configuration
-  __shared__ MtConst mc[4];
-  const float a = p.acc[size_t(b) * 100 + h], st = p.steer[size_t(b) * 100 + h];
-  if (threadIdx.x < 4) {  // alphas 2|a|, 5|a|, 2|s|, 5|s| of this (candidate, step)
-    const float f = threadIdx.x < 2 ? fabsf(a) : fabsf(st);
-    mc[threadIdx.x] = mt_const(double((threadIdx.x & 1 ? 5.0f : 2.0f) * f));
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = blockIdx.x * kBetaRows + lane, h = blockIdx.y;
+  const int groups = (p.B + kBetaCands - 1) / kBetaCands;
+  const int g = blockIdx.z / groups, j0 = (blockIdx.z - g * groups) * kBetaCands;  // configuration, first candidate
+  const int nc = min(kBetaCands, p.B - j0);
+  const double* gtab_ = p.gtab + size_t(g) * gtab_stride(S, H);
+  const size_t plane = size_t(S) * H, at = size_t(h) * S + r, sl = size_t(kGammaTabAttempts) * 4 * plane;
+  __shared__ double tx[4][kBetaRows], tlu[4][kBetaRows], tlw[4][kBetaRows];
+  __shared__ MtConst mc[kBetaCands][4];
+  __shared__ float fab[kBetaCands][2];
+  {  // wave w stages gamma stream w (acc A, acc B, steer A, steer B)
+    const double* tw = gtab_ + w * sl + size_t(h) * S + min(r, S - 1);
+    tx[w][lane] = tw[0];
+    tlu[w][lane] = tw[2 * plane];
+    tlw[w][lane] = tw[3 * plane];
+  }
+  if (threadIdx.x < 4 * kBetaCands) {  // alphas 2|a|, 5|a|, 2|s|, 5|s| of each candidate at this step
+    const int c = threadIdx.x >> 2, i = threadIdx.x & 3;
+    const size_t b = size_t(g) * p.B + j0 + min(c, nc - 1);
+    const float f = fabsf(i < 2 ? p.acc[b * 100 + h] : p.steer[b * 100 + h]);
+    mc[c][i] = mt_const(double((i & 1 ? 5.0f : 2.0f) * f));
+    if ((i & 1) == 0) fab[c][i >> 1] = f;
   }
   __syncthreads();
   if (r >= S) return;
-  // table-only fast path; the rare rest (more than the tabulated attempts)
-  // is deferred to k_beta_fix so this kernel does not carry that code's registers
-  const size_t sl = size_t(kGammaTabAttempts) * 4 * S * H;
-  const float fa = fabsf(a), fs = fabsf(st);
-  float nba, nbs;
-  const bool ok = beta_draw_fast(double(2.0f * fa), double(5.0f * fa), 2.0, 5.0, mc[0], mc[1], gtab, gtab + sl,
-                                 S, H, r, h, nba) &&
-                  beta_draw_fast(double(2.0f * fs), double(5.0f * fs), 2.0, 5.0, mc[2], mc[3], gtab + 2 * sl,
-                                 gtab + 3 * sl, S, H, r, h, nbs);
-  if (!ok) {
-    const unsigned slot = atomicAdd(p.bfix_n, 1u);
-    p.bfix[slot] = (uint32_t(b) * uint32_t(H) + uint32_t(h)) * uint32_t(S) + uint32_t(r);
-    return;
+  // one gamma pair (streams k, k + 1: acc or steer) of candidate c -> its Beta draw
+  auto draw = [&](int c, int k, float f, float& out) {
+    double ga, ua, gb, ub;
+    // the fallback's table pointer laundered per call: its (loop-invariant)
+    // loads must not be hoisted out of the candidate loop (72 registers)
+    const double* gtab = gtab_;
+    __asm__ volatile("" : "+s"(gtab));
+    const bool ok = (tab_try(mc[c][k], TabAtt{tx[k][lane], tlu[k][lane], tlw[k][lane]}, ga, ua) ||
+                     gamma_tab_from(mc[c][k], gtab + k * sl, plane, at, 1, ga, ua)) &&
+                    (tab_try(mc[c][k + 1], TabAtt{tx[k + 1][lane], tlu[k + 1][lane], tlw[k + 1][lane]}, gb, ub) ||
+                     gamma_tab_from(mc[c][k + 1], gtab + (k + 1) * sl, plane, at, 1, gb, ub));
+    if (ok) out = beta_combine(double(2.0f * f), double(5.0f * f), 2.0, 5.0, ga, ua, gb, ub);
+    return ok;
+  };
+#pragma unroll 1
+  for (int c = w; c < nc; c += 4) {
+    const uint32_t b = uint32_t(g) * p.B + j0 + c;
+    float* o = p.bplane + size_t(b) * 2 * H * S;
+    float nba, nbs;
+    if (draw(c, 0, fab[c][0], nba) && draw(c, 2, fab[c][1], nbs)) {
+      o[size_t(h) * S + r] = nba;
+      o[(size_t(H) + h) * S + r] = nbs;
+    } else {  // more attempts than tabulated (rare): the full sampler in k_beta_fix
+      const unsigned slot = atomicAdd(p.bfix_n, 1u);
+      p.bfix[slot] = (b * uint32_t(H) + uint32_t(h)) * uint32_t(S) + uint32_t(r);
+    }
   }
-  float* o = p.bplane + size_t(b) * 2 * H * S;
-  o[size_t(h) * S + r] = nba;
-  o[(size_t(H) + h) * S + r] = nbs;
 }
 
 // the deferred elements of k_beta_planes, through the full sampler
@@ -213,7 +261,8 @@ __global__ __launch_bounds__(256) void k_beta_fix(Params p, int t) {
 }  // namespace
 
 void launch_beta_planes(const Params& p, int t, hipStream_t s) {
-  hipLaunchKernelGGL(k_beta_planes, dim3((p.S + 255) / 256, p.H, p.Bt), dim3(256), 0, s, p, t);
+  const int groups = (p.B + kBetaCands - 1) / kBetaCands;
+  hipLaunchKernelGGL(k_beta_planes, dim3((p.S + kBetaRows - 1) / kBetaRows, p.H, p.G * groups), dim3(256), 0, s, p, t);
   hipLaunchKernelGGL(k_beta_fix, dim3(256), dim3(256), 0, s, p, t);
 }
 

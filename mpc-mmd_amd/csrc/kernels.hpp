@@ -34,6 +34,9 @@ HDI_CONST int pos_pad(int M) { return ((M + 1) + 31) & ~31; }  // whole pairs of
 // (k_bkernel: a wave holds a row as one float4 per lane and block); pad
 // columns hold +inf
 HDI_CONST int dist_stride(int M) { return (M + 255) & ~255; }
+// floats per sample of Params::bkred: the n (n - 1) / 2 strict lower triangle
+// rounded to whole 16-byte groups (the QP kernel stages rows as float4)
+HDI_CONST int tri_stride(int n) { return ((n * (n - 1) / 2) + 3) & ~3; }
 
 struct Params {
   // shapes / configuration.  A launch covers G configurations of B
@@ -107,17 +110,14 @@ struct Params {
   int32_t* bimin;          // [B] argmin sample of the last beta-iteration
   double* genm;            // [B][pos_pad(M)]  fp32-rounded elite mean, as fp64 (pad 0)
   int32_t* bestsel;        // [B][n]       reduced set of the best sample
-  double* brow;            // [B][100][n]  K_mixed row sums (fp64)
-  float* bkred;            // [B][100][n(n-1)/2] K_red strict lower triangle
+  float* brow;             // [B][100][n]  K_mixed row sums (fp32 partial sums, the reference's precision)
+  float* bkred;            // [B][100][tri_stride(n)] K_red strict lower triangle (entry (k, kk < k) at k (k-1)/2 + kk)
   float* ygen;             // [B][kBzCols][ygs] new samples of the current beta-iteration (ygs = M+1 rounded to 32)
   // phase timestamps (s_memrealtime, 100 MHz) of workgroup 0, for profiling
   unsigned long long* dbg;  // [64]
   // work counters for the roofline, summed over k_bkernel workgroups:
   // [0] distinct distance rows staged, [1] (sample, reduced row) pairs summed
   unsigned long long* stats;  // [8]
-  // per-workgroup (start, end) stamps of the last k_bkernel launch, written
-  // only by builds with -DMPCMMD_WGT (scheduling experiments)
-  unsigned long long* wgt;    // [8 Bt][2]
   // outputs
   float* results;          // [G][T][kResultStride]
   int32_t* tr_proj;        // [G][T][B]

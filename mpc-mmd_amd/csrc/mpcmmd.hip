@@ -486,8 +486,8 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
       p.phib = (double*)h->alloc("phib", BT * ((h->M + 1 + 15) / 16) * 66 * 8);
       p.bimin = (int32_t*)h->alloc("bimin", BT * 4);
       p.bestsel = (int32_t*)h->alloc("bestsel", BT * n * 4);
-      p.brow = (double*)h->alloc("brow", BT * kBetaSamples * n * 8);
-      p.bkred = (float*)h->alloc("bkred", BT * kBetaSamples * (n * (n - 1) / 2) * 4);
+      p.brow = (float*)h->alloc("brow", BT * kBetaSamples * n * 4);
+      p.bkred = (float*)h->alloc("bkred", BT * kBetaSamples * tri_stride(int(n)) * 4);
       p.ygen = (float*)h->alloc("ygen", BT * kBzCols * ygen_stride(h->M) * 4);
     }
     p.pop = (float*)h->alloc("pop", size_t(2) * BT * 8 * 4);
@@ -510,7 +510,6 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     p.btrace = (float*)h->alloc("btrace", BT * kBetaIters * 4);
     p.dbg = (unsigned long long*)h->alloc("dbg", 64 * 8);
     p.stats = (unsigned long long*)h->alloc("stats", 8 * 8);
-    p.wgt = (unsigned long long*)h->alloc("wgt", BT * 8 * 2 * 8);
     p.results = (float*)h->alloc("results", size_t(GM) * T * kResultStride * 4);
     p.tr_proj = (int32_t*)h->alloc("tr_proj", size_t(GM) * T * B * 4);
     p.tr_obs = (int32_t*)h->alloc("tr_obs", size_t(GM) * T * kEliteCost * 4);

@@ -139,21 +139,27 @@ HDI MtConst mt_const(double alpha) {
   const double d = a1 - 1.0 / 3.0;
   return MtConst{d, 1.0 / sqrt(9.0 * d)};
 }
-// One tabulated attempt t (fields x, u, log u, +-log w at stride plane):
+// One tabulated attempt (fields x, log u, +-log w; the uniform u itself is
+// only needed by the squeeze, whose decision the sign of log w holds):
 // Marsaglia-Tsang acceptance with the stored squeeze decision
-DEVI bool tab_attempt(MtConst mc, const double* t, size_t plane, double& g, double& lub) {
-  const double x = t[0];
-  const double v = 1.0 + mc.c * x;
+struct TabAtt {
+  double x, lu, lw;
+};
+DEVI TabAtt tab_load(const double* t, size_t plane) { return TabAtt{t[0], t[2 * plane], t[3 * plane]}; }
+DEVI bool tab_try(MtConst mc, const TabAtt& a, double& g, double& lub) {
+  const double v = 1.0 + mc.c * a.x;
   if (v > 0.0) {
     const double v3 = v * v * v;
-    const double lw = t[3 * plane];
-    if (lw < 0.0 || mt_log_test(x, t[2 * plane], mc.d, v3)) {
+    if (a.lw < 0.0 || mt_log_test(a.x, a.lu, mc.d, v3)) {
       g = mc.d * v3;
-      lub = -fabs(lw);
+      lub = -fabs(a.lw);
       return true;
     }
   }
   return false;
+}
+DEVI bool tab_attempt(MtConst mc, const double* t, size_t plane, double& g, double& lub) {
+  return tab_try(mc, tab_load(t, plane), g, lub);
 }
 DEVI void gamma_parts_tab(MtConst mc, const double* tab, int S, int H, int r, int h, uint32_t k0, uint32_t k1,
                           uint32_t stream, uint32_t elem, double& g, double& lub) {
@@ -213,44 +219,12 @@ DEVI float beta_draw_tab(double a, double b, double ra, double rb, MtConst mc_a,
   return beta_combine(a, b, ra, rb, ga, ua, gb, ub);
 }
 
-// Table-only fast path of beta_draw_tab for the hot plane kernel: returns
-// false (and leaves `out`) when a gamma needs more than the tabulated
-// attempts (rare); the caller then defers
-// the element to the full beta_draw_tab (identical arithmetic).
-// attempts k0 .. kGammaTabAttempts - 1 of the table
+// Table-only path for the hot plane kernel: attempts k0 .. kGammaTabAttempts
+// - 1 of the table; false when a gamma needs more (rare: the caller defers
+// the element to the full beta_draw_tab, identical arithmetic)
 DEVI bool gamma_tab_from(MtConst mc, const double* tab, size_t plane, size_t at, int k0, double& g, double& lub) {
   for (int k = k0; k < kGammaTabAttempts; ++k)
     if (tab_attempt(mc, tab + size_t(k) * 4 * plane + at, plane, g, lub)) return true;
   return false;
 }
-DEVI bool gamma_tab_only(MtConst mc, const double* tab, size_t plane, size_t at, double& g, double& lub) {
-  return gamma_tab_from(mc, tab, plane, at, 0, g, lub);
-}
-// One tabulated attempt held in registers (k_beta_planes: loaded once per
-// (row, step) and applied to several candidates' alphas).
-struct GammaAtt {
-  double x, u, lu, lw;
-};
-DEVI bool gamma_try(MtConst mc, const GammaAtt& t, double& g, double& lub) {
-  const double v = 1.0 + mc.c * t.x;
-  if (v > 0.0) {
-    const double v3 = v * v * v;
-    if (mt_accept(t.x, t.u, t.lu, mc.d, v3)) {
-      g = mc.d * v3;
-      lub = t.lw;
-      return true;
-    }
-  }
-  return false;
-}
-DEVI bool beta_draw_fast(double a, double b, double ra, double rb, MtConst mc_a, MtConst mc_b, const double* tab_a,
-                         const double* tab_b, int S, int H, int r, int h, float& out) {
-  const size_t plane = size_t(S) * H, at = size_t(h) * S + r;
-  double ga, ua, gb, ub;
-  if (!gamma_tab_only(mc_a, tab_a, plane, at, ga, ua) || !gamma_tab_only(mc_b, tab_b, plane, at, gb, ub))
-    return false;
-  out = beta_combine(a, b, ra, rb, ga, ua, gb, ub);
-  return true;
-}
-
 }  // namespace mpcmmd

@@ -8,6 +8,7 @@ namespace mpcmmd {
 
 constexpr float kDt = 0.15f;         // cem.py:40
 constexpr float kWheelBase = 2.5f;   // cem.py:26
+constexpr float kObsA = 4.25f;       // a_obs (cem.py:25)
 
 // The two Beta draws of (candidate controls a, s; row r, step h)
 // (cem_helper.py:427-433): Beta(2|a|, 5|a|), Beta(2|s|, 5|s|).  mc: the four
@@ -63,6 +64,22 @@ DEVI void noisy_control(const Params& p, const Cfg& cf, int t, int r, int h, flo
   sn = (s + sp) + p.steer_const * nc;
 }
 
+// The same perturbation from the step's noise values already in registers:
+// gaussian n0, n1 = the acc / steer normals, beta n0, n1 = the two Beta
+// draws; n2 = the const-noise normal (identical arithmetic to noisy_control)
+DEVI void noisy_from(const Params& p, float a, float s, float n0, float n1, float n2, float& an, float& sn) {
+  float ap, sp;
+  if (p.noise == 0) {
+    ap = (p.sigma_acc * fabsf(a)) * n0;
+    sp = (p.sigma_steer * fabsf(s)) * n1;
+  } else {
+    ap = p.sigma_acc * (2.0f * n0 - 1.0f);
+    sp = p.K_steer * (2.0f * n1 - 1.0f);  // K_steer holds float32(K_steer * sigma_steer)
+  }
+  an = (a + ap) + p.acc_const * n2;
+  sn = (s + sp) + p.steer_const * n2;
+}
+
 // compute_rollout_one_step (cem_helper.py:380-400), fp32 in reference order.
 // psidot = v tan(steer) / 2.5: division by 2.5 via the exact fma form.
 DEVI void bicycle_step(float& x, float& y, float& vx, float& vy, float& psi, float an, float sn) {
@@ -70,8 +87,10 @@ DEVI void bicycle_step(float& x, float& y, float& vx, float& vy, float& psi, flo
   v = v + an * kDt;
   const float psidot = div_rc(v * tanf(sn), kWheelBase, 1.0f / kWheelBase);
   psi = psi + psidot * kDt;
-  vx = v * cosf(psi);
-  vy = v * sinf(psi);
+  float sp, cp;
+  sincosf(psi, &sp, &cp);  // one argument reduction for both (OCML: the values of sinf / cosf)
+  vx = v * cp;
+  vy = v * sp;
   x = x + vx * kDt;
   y = y + vy * kDt;
 }

@@ -28,21 +28,7 @@ def main():
         h.iterate(t, 1)
     h.sync()
     d = h.read("dbg", np.uint64).astype(np.int64)
-    wgt = h.read("wgt", np.uint64).astype(np.int64).reshape(-1, 2)
     h.close()
-    wgt = wgt[(wgt[:, 0] > 0) & (wgt[:, 1] > wgt[:, 0])]
-    if len(wgt):  # -DMPCMMD_WGT build: every k_bkernel workgroup's (start, end)
-        t0 = wgt[:, 0].min()
-        st, en = (wgt[:, 0] - t0) / 100.0, (wgt[:, 1] - t0) / 100.0
-        dur = en - st
-        ev = sorted([(x, 1) for x in st] + [(x, -1) for x in en])
-        cur = peak = 0
-        for _, e in ev:
-            cur += e
-            peak = max(peak, cur)
-        print(f"bkernel workgroups {len(wgt)}: span {en.max():.1f} us, duration min/median/max "
-              f"{dur.min():.1f}/{np.median(dur):.1f}/{dur.max():.1f} us, peak concurrency {peak}, "
-              f"started by 5 us {int((st < 5).sum())}, start quantiles {np.percentile(st, [25, 50, 75, 100]).round(1)}")
     us = lambda a, b: (d[b] - d[a]) / 100.0  # noqa: E731  (100 MHz ticks -> us)
     print(f"{name}: bsample {us(0, 1):.1f} us")
     print(f"bkernel: setup {us(16, 17):.1f} us, rows {us(17, 20):.1f} us, total {us(16, 20):.1f} us")
