@@ -502,11 +502,17 @@ DEVI void select_walk(Row row, Out out, int first, int last, int stride, int M, 
 //   A: A[r][h]   B: B[h][r]   C/D register i: C[h + 4 i][r]
 typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int kSampleTiles = kBzCols / 16;  // 6 tiles of 16 sample columns (89 used)
-constexpr int kTilesPerWave = 6;
-constexpr int kSampleWaves = kSampleTiles / kTilesPerWave;
-static_assert(kSampleTiles % kTilesPerWave == 0, "tiles per wave");
-static_assert(kTilesPerWave % 2 == 0, "sample tiles are loaded in pairs");
 static_assert(kBzCols >= kNew, "sample tiles");
+// TPW = sample tiles per wave: 6 (one wave per candidate: the generator
+// operands loaded once) when the batch fills the chip, else 2 or 1 (3 or 6
+// waves per candidate, each loading the block's generators itself) so a
+// small batch -- the reference's num_batch = 100 -- still spreads over the
+// SIMDs
+template <int TPW>
+constexpr int sample_waves() {
+  static_assert(kSampleTiles % TPW == 0, "tiles per wave");
+  return kSampleTiles / TPW;
+}
 
 DEVI d4 mfma64(double a, double b, d4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
 
@@ -514,16 +520,18 @@ DEVI d4 mfma64(double a, double b, d4 c) { return __builtin_amdgcn_mfma_f64_16x1
 // normals are zero padded to whole blocks and tiles; features >= 11 masked
 // by selects), so the loop has no branches and the compiler can count
 // outstanding loads exactly.
+template <int TPW>
 struct SampleBlock {
   double wA[4];  // W[p0 + 4k + h][r]        (A of W^T Z; r = feature)
   double wX[3];  // W[p0 + r][4i + h]        (A of W U^T; 4i + h = feature)
   double uX[3];  // U[p0 + r][4i + h]        (B of W U^T, A of U S)
   double L;      // L_jj of position p0 + r
   double m[4];   // mean of position p0 + h + 4i
-  double z[kTilesPerWave][4];  // Z[p0 + 4k + h][sample of (tile t, lane r)] (sample_of)
+  double z[TPW][4];  // Z[p0 + 4k + h][sample of (tile t, lane r)] (sample_of)
 };
 
-DEVI void load_block(SampleBlock& q, const double* G, const double* gm, const double* z, int p0, int s0, int r,
+template <int TPW>
+DEVI void load_block(SampleBlock<TPW>& q, const double* G, const double* gm, const double* z, int p0, int s0, int r,
                      int h) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) q.wA[k] = G[size_t(p0 + 4 * k + h) * kGenStride + kGenW + r];  // rows >= 11 of S unused
@@ -537,15 +545,22 @@ DEVI void load_block(SampleBlock& q, const double* G, const double* gm, const do
 #pragma unroll
   for (int i = 0; i < 4; ++i) q.m[i] = gm[p0 + h + 4 * i];
   // tiles in pairs: lane r of tiles 2u, 2u + 1 takes samples 32u + 2r, 32u +
-  // 2r + 1, so one 16-byte load fetches both B operands
+  // 2r + 1, so one 16-byte load fetches both B operands (one tile per wave:
+  // lane r takes sample 16 w + r)
+  if constexpr (TPW == 1) {
 #pragma unroll
-  for (int u = 0; u < kTilesPerWave / 2; ++u)
+    for (int k = 0; k < 4; ++k) q.z[0][k] = z[size_t(p0 + 4 * k + h) * kBzCols + s0 + r];
+  } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const double2 zz = *reinterpret_cast<const double2*>(z + size_t(p0 + 4 * k + h) * kBzCols + s0 + 32 * u + 2 * r);
-      q.z[2 * u][k] = zz.x;
-      q.z[2 * u + 1][k] = zz.y;
-    }
+    for (int u = 0; u < TPW / 2; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double2 zz =
+            *reinterpret_cast<const double2*>(z + size_t(p0 + 4 * k + h) * kBzCols + s0 + 32 * u + 2 * r);
+        q.z[2 * u][k] = zz.x;
+        q.z[2 * u + 1][k] = zz.y;
+      }
+  }
 }
 
 // One block's MFMAs for the wave's tiles, all accumulating in place:
@@ -555,7 +570,8 @@ DEVI void load_block(SampleBlock& q, const double* G, const double* gm, const do
 // Tiles are interleaved, so every accumulator chain has 6 MFMAs between
 // dependent steps.  No VALU work on the accumulators: the pipe never waits
 // for a vector add between blocks.
-DEVI void block_mfma(const SampleBlock& cur, d4* S, d4* Y, int r, int h) {
+template <int TPW>
+DEVI void block_mfma(const SampleBlock<TPW>& cur, d4* S, d4* Y, int r, int h) {
   d4 X = d4{0.0, 0.0, 0.0, 0.0};  // X = W_c U_c^T: register i holds w_{h+4i} . u_r = T[row r][col h + 4i]
 #pragma unroll
   for (int i = 0; i < 3; ++i) X = mfma64(cur.wX[i], cur.uX[i], X);
@@ -563,11 +579,11 @@ DEVI void block_mfma(const SampleBlock& cur, d4* S, d4* Y, int r, int h) {
 #pragma unroll
   for (int k = 0; k < 3; ++k)
 #pragma unroll
-    for (int t = 0; t < kTilesPerWave; ++t) Y[t] = mfma64(cur.uX[k], S[t][k], k == 0 ? m : Y[t]);
+    for (int t = 0; t < TPW; ++t) Y[t] = mfma64(cur.uX[k], S[t][k], k == 0 ? m : Y[t]);
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
-    for (int t = 0; t < kTilesPerWave; ++t) S[t] = mfma64(cur.wA[k], cur.z[t][k], S[t]);
+    for (int t = 0; t < TPW; ++t) S[t] = mfma64(cur.wA[k], cur.z[t][k], S[t]);
   double T[4];  // A operand of T Z, k-step i: T[r][4i + h]
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -577,7 +593,7 @@ DEVI void block_mfma(const SampleBlock& cur, d4* S, d4* Y, int r, int h) {
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
-    for (int t = 0; t < kTilesPerWave; ++t) Y[t] = mfma64(T[k], cur.z[t][k], Y[t]);
+    for (int t = 0; t < TPW; ++t) Y[t] = mfma64(T[k], cur.z[t][k], Y[t]);
 }
 
 // the finished block's samples to fp32 (the sigma coordinate M clipped)
@@ -585,9 +601,10 @@ DEVI void block_mfma(const SampleBlock& cur, d4* S, d4* Y, int r, int h) {
 // across (lane row, register) -- a block swap by permlane32, then the 2 x 2
 // blocks by permlane16 -- leaves positions p0 + 4h .. p0 + 4h + 3 in lane row
 // h, stored as one 16-byte write per tile.
+template <int TPW>
 DEVI void block_store(const d4* Yv, float* Y, int p0, int M, int ys, int h) {
 #pragma unroll
-  for (int t = 0; t < kTilesPerWave; ++t) {
+  for (int t = 0; t < TPW; ++t) {
     float v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = p0 + h + 4 * i == M ? fmaxf(float(Yv[t][i]), 0.01f) : float(Yv[t][i]);
@@ -595,32 +612,33 @@ DEVI void block_store(const d4* Yv, float* Y, int p0, int M, int ys, int h) {
     permlane_swap<32>(v[1], v[3]);
     permlane_swap<16>(v[0], v[1]);
     permlane_swap<16>(v[2], v[3]);
-    // sample s0 + 32 (t / 2) + 2 r + t % 2
-    float4* yrow = reinterpret_cast<float4*>(Y + size_t(32 * (t >> 1) + (t & 1)) * ys + p0 + 4 * h);
+    // sample s0 + 32 (t / 2) + 2 r + t % 2 (one tile per wave: s0 + r)
+    float4* yrow = reinterpret_cast<float4*>(Y + size_t(TPW == 1 ? 0 : 32 * (t >> 1) + (t & 1)) * ys + p0 + 4 * h);
     *yrow = make_float4(v[0], v[1], v[2], v[3]);
   }
 }
 
-__global__ __launch_bounds__(64 * kSampleWaves) void k_bsample(Params p, int tb) {
+template <int TPW>
+__global__ __launch_bounds__(64 * sample_waves<TPW>()) void k_bsample(Params p, int tb) {
   const int b = p.b0 + blockIdx.x, M = p.M, Pp = pos_pad(M);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, h = lane >> 4;
-  const int s0 = w * kTilesPerWave * 16;
+  const int s0 = w * TPW * 16;
   MPCMMD_STAMP(p, 0);
   const double* G = p.gen + size_t(b) * Pp * kGenStride;
   const double* gm = p.genm + size_t(b) * Pp;
   const double* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
   const int ys = ygen_stride(M);
-  float* Y = p.ygen + (size_t(b) * kBzCols + s0 + 2 * r) * ys;
-  d4 S[kTilesPerWave], Ya[kTilesPerWave], Yb[kTilesPerWave];
+  float* Y = p.ygen + (size_t(b) * kBzCols + s0 + (TPW == 1 ? r : 2 * r)) * ys;
+  d4 S[TPW], Ya[TPW], Yb[TPW];
 #pragma unroll
-  for (int t = 0; t < kTilesPerWave; ++t) S[t] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int t = 0; t < TPW; ++t) S[t] = d4{0.0, 0.0, 0.0, 0.0};
   const int nblk = Pp >> 4;
   // blocks in pairs, operands and outputs ping-ponged: the next block's loads
   // are in flight and its MFMAs issued while the previous block's samples
   // are converted and stored (the last prefetch re-reads a block; nblk is
   // even; sched barriers keep that order)
-  SampleBlock qa, qb;
+  SampleBlock<TPW> qa, qb;
   load_block(qa, G, gm, z, 0, s0, r, h);
   for (int c = 0; c < nblk; c += 2) {
     const int p0 = c << 4;
@@ -628,16 +646,16 @@ __global__ __launch_bounds__(64 * kSampleWaves) void k_bsample(Params p, int tb)
     __builtin_amdgcn_sched_barrier(0);
     block_mfma(qa, S, Ya, r, h);
     __builtin_amdgcn_sched_barrier(0);
-    if (c > 0) block_store(Yb, Y, p0 - 16, M, ys, h);
+    if (c > 0) block_store<TPW>(Yb, Y, p0 - 16, M, ys, h);
     __builtin_amdgcn_sched_barrier(0);
     load_block(qa, G, gm, z, min(p0 + 32, Pp - 16), s0, r, h);
     __builtin_amdgcn_sched_barrier(0);
     block_mfma(qb, S, Yb, r, h);
     __builtin_amdgcn_sched_barrier(0);
-    block_store(Ya, Y, p0, M, ys, h);
+    block_store<TPW>(Ya, Y, p0, M, ys, h);
     __builtin_amdgcn_sched_barrier(0);
   }
-  block_store(Yb, Y, Pp - 16, M, ys, h);
+  block_store<TPW>(Yb, Y, Pp - 16, M, ys, h);
   MPCMMD_STAMP(p, 1);
 }
 
@@ -714,7 +732,11 @@ struct KerLds {
 
 // persistent: sel (short), csg, pairs (K_red offset | k << 18 | s << 24), the distinct rows
 // and their first pair; the setup's counts / fill / scan (10 M bytes) overlay
-// the wave row buffers
+// the wave row buffers.  Rows longer than kRowLdsMaxV4 float4s per lane are
+// not copied to LDS (the K_red gathers read the row from global memory, L2-hot
+// from the wave's own load): 16 waves per workgroup also at M = 2500.
+constexpr int kRowLdsMaxV4 = 4;
+HDI bool row_in_lds(int M) { return (dist_stride(M) >> 8) <= kRowLdsMaxV4; }
 HDI KerLds ker_lds(int M, int n, int waves) {
   KerLds L{};
   size_t o = 0;
@@ -731,7 +753,7 @@ HDI KerLds ker_lds(int M, int n, int waves) {
   L.order = take(size_t(M) * 2);
   L.bins = take(kLptBins * 4);
   L.misc = take(32 * 4);  // [0] next row, [1] distinct rows, [16..31] scan wave totals
-  const size_t rb = size_t(waves) * dist_stride(M) * 4, setup = size_t(M) * 10;
+  const size_t rb = row_in_lds(M) ? size_t(waves) * dist_stride(M) * 4 : 0, setup = size_t(M) * 10;
   L.rowbuf = take(rb > setup ? rb : setup);
   L.total = o;
   return L;
@@ -908,9 +930,14 @@ __global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb,
   // one distinct row u held in x: its pairs 8 at a time, row sums and then
   // the batch's K_red entries (8 lanes per pair, kk = lane & 7 + 8 i)
   auto do_row = [&](const float4 (&x)[NV4], int u) {
+    const float* rg = rb;  // the row the K_red gathers read: the wave's LDS copy, or the global row
+    if constexpr (NV4 <= kRowLdsMaxV4) {
 #pragma unroll
-    for (int t = 0; t < NV4; ++t) rb4[lane + 64 * t] = x[t];
-    wave_sync();  // the row copy is in LDS before the gathers (one wave's LDS operations run in order)
+      for (int t = 0; t < NV4; ++t) rb4[lane + 64 * t] = x[t];
+      wave_sync();  // the row copy is in LDS before the gathers (one wave's LDS operations run in order)
+    } else {
+      rg = reinterpret_cast<const float*>(Dg + size_t(ulist[u]) * (Md >> 2));
+    }
     const int pb = ustart[u], pc = ustart[u + 1] - pb;
     for (int c0 = 0; c0 < pc; c0 += 64) {  // (rows with more than 64 pairs: chunks)
       // lane l holds pair c0 + l and its scale; batches broadcast them by readlane
@@ -948,7 +975,7 @@ __global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb,
         if ((lane & 7) == 4 && live) rowsum[s * n + k] = sum;
         const short* sls = sl + s * n;
         float* kr = kbase + (pkj & 0x3FFFFu);
-        for (int kk = lane & 7; kk < k; kk += 8) kr[kk] = __builtin_amdgcn_exp2f(rb[sls[kk]] * cj);
+        for (int kk = lane & 7; kk < k; kk += 8) kr[kk] = __builtin_amdgcn_exp2f(rg[sls[kk]] * cj);
       }
     }
     wave_sync();  // the gathers read the copy before the next row overwrites it
@@ -1214,10 +1241,12 @@ DEVI void bqp_quad(const Params& p, int tb, float* kl) {
 }
 
 HDI int qp_np(int n) { return n <= 8 ? 8 : (n <= 16 ? 16 : (n <= 24 ? 24 : (n <= 32 ? 32 : (n <= 48 ? 48 : 64)))); }
-constexpr int kQpThreads = 128;  // 32 QPs per workgroup (their K_red in LDS: 30 KB at n = 22)
+// threads per workgroup: 32 QPs (their K_red in LDS: 30 KB at n = 22), 16 QPs
+// for n > 24 (32 KB at n = 32, so the LDS still admits 4 workgroups per CU)
+HDI_CONST int qp_threads(int np) { return np > 24 ? 64 : 128; }
 
 template <int NP>
-__global__ __launch_bounds__(kQpThreads, NP == 24 ? 3 : (NP <= 16 ? 4 : 2)) void k_bqp(Params p, int tb) {
+__global__ __launch_bounds__(qp_threads(NP), NP == 24 ? 3 : (NP <= 16 ? 4 : 2)) void k_bqp(Params p, int tb) {
   extern __shared__ __attribute__((aligned(16))) float kl[];
   bqp_quad<NP>(p, tb, kl);
 }
@@ -1765,7 +1794,15 @@ void launch_bdist(const Params& p, hipStream_t s) {
 }
 
 void launch_bsample(const Params& p, int tb, hipStream_t s) {
-  hipLaunchKernelGGL(k_bsample, dim3(p.nb), dim3(64 * kSampleWaves), 0, s, p, tb);
+  // one wave per candidate when the launch alone holds >= ~half a wave per
+  // SIMD; smaller batches split the sample tiles over 3 waves (num_batch =
+  // 100: 7.9 -> 3.9 ms per step) or, below 60 candidates, 6
+  if (p.nb >= 384)
+    hipLaunchKernelGGL((k_bsample<6>), dim3(p.nb), dim3(64 * sample_waves<6>()), 0, s, p, tb);
+  else if (p.nb >= 60)
+    hipLaunchKernelGGL((k_bsample<2>), dim3(p.nb), dim3(64 * sample_waves<2>()), 0, s, p, tb);
+  else
+    hipLaunchKernelGGL((k_bsample<1>), dim3(p.nb), dim3(64 * sample_waves<1>()), 0, s, p, tb);
 }
 
 // waves per candidate: ~16 single-wave workgroups per SIMD over the launch,
@@ -1810,24 +1847,25 @@ void launch_bselect(const Params& p, int tb, hipStream_t s) {
   return launch_bselect_q<64>(p, tb, s);
 }
 
+template <int NP>
+void launch_bqp_quad(const Params& p, int tb, int qps, hipStream_t s) {
+  constexpr int T = qp_threads(NP);
+  const size_t lds = size_t(T / 4) * tri_stride(p.n) * 4;
+  hipLaunchKernelGGL((k_bqp<NP>), dim3((qps * 4 + T - 1) / T), dim3(T), lds, s, p, tb);
+}
+
 void launch_bqp(const Params& p, int tb, hipStream_t s) {
   const int qps = p.nb * (kBetaSamples - first_sample(tb));
-  const dim3 grid((qps * 4 + kQpThreads - 1) / kQpThreads);
   const dim3 grid_wave((qps + 3) / 4);
-  const size_t lds = size_t(kQpThreads / 4) * tri_stride(p.n) * 4;
   switch (qp_np(p.n)) {
     case 8:
-      hipLaunchKernelGGL((k_bqp<8>), grid, dim3(kQpThreads), lds, s, p, tb);
-      return;
+      return launch_bqp_quad<8>(p, tb, qps, s);
     case 16:
-      hipLaunchKernelGGL((k_bqp<16>), grid, dim3(kQpThreads), lds, s, p, tb);
-      return;
+      return launch_bqp_quad<16>(p, tb, qps, s);
     case 24:
-      hipLaunchKernelGGL((k_bqp<24>), grid, dim3(kQpThreads), lds, s, p, tb);
-      return;
+      return launch_bqp_quad<24>(p, tb, qps, s);
     case 32:
-      hipLaunchKernelGGL((k_bqp<32>), grid, dim3(kQpThreads), lds, s, p, tb);
-      return;
+      return launch_bqp_quad<32>(p, tb, qps, s);
     case 48:
       hipLaunchKernelGGL((k_bqp_wave<48>), grid_wave, dim3(256), 0, s, p, tb);
       return;

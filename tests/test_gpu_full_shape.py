@@ -1,6 +1,9 @@
 """GPU parity at the BASELINE shapes themselves (not only the small lockstep
-shapes): configs[1] (mmd_opt, B=1024, H=30, O=10, n=22 -> 484 mother rollouts)
-and configs[2] (cvar, B=1024, S=500, beta noise 0.3).  One outer iteration
+shapes): configs[1] (mmd_opt, B=1024, H=30, O=10, n=22 -> 484 mother rollouts),
+configs[2] (cvar, B=1024, S=500, beta noise 0.3) and configs[3]'s per-candidate
+shape (synthetic_dynamic_obs: H=50, O=20 QP obstacle tracks, n=32 -> 1024
+mother rollouts, y_lb, y_ub = -2.25, -1.25 and K_steer = 0.05 of
+D/optimizer/cem.py:155, cem_helper.py:24; 64 candidates).  One outer iteration
 stage by stage on identical inputs: the front for all 1024 candidates, the
 risk stage for a sample of candidates (the oracle's beta-CEM costs ~0.4 s per
 candidate), the selection (elite index sets exact) and the next population.
@@ -15,15 +18,23 @@ from test_gpu_parity_baseline import _sync_state
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("cost,noise,n,sample", [("mmd_opt", "gaussian", 22, list(range(0, 1024, 64))),
-                                                 ("cvar", "beta", 500, list(range(0, 1024, 64)))])
-def test_full_shape_iteration(native, cost, noise, n, sample):
-    B, O, H = 1024, 10, 30
-    ora, nat, xo, yo = make_pair(native, cost, noise, n=n, O=O, H=H, B=B, T=1)
+@pytest.mark.parametrize("cost,noise,n,sample,B,O,H,variant", [
+    ("mmd_opt", "gaussian", 22, list(range(0, 1024, 64)), 1024, 10, 30, "static"),
+    ("cvar", "beta", 500, list(range(0, 1024, 64)), 1024, 10, 30, "static"),
+    ("mmd_opt", "gaussian", 32, [0, 9, 31, 50, 63], 64, 20, 50, "dynamic")])
+def test_full_shape_iteration(native, cost, noise, n, sample, B, O, H, variant):
+    ora, nat, xo, yo = make_pair(native, cost, noise, n=n, O=O, H=H, B=B, T=1, variant=variant)
+    if variant == "dynamic":  # the synthetic_dynamic_obs driver's QP obstacle tracks (library generator)
+        from optimizer.obs_data_generate_dynamic import dynamic_obstacles
+        dyn = dynamic_obstacles(3, O)
+        xo, yo = dyn["x_traj"], dyn["y_traj"]
+    init = DEFAULT_INIT.copy()
+    if variant == "dynamic":
+        init[1] = -1.75   # D/main_mpc.py:38
     draws = oracle.Draws.random(ora.prob, np.random.default_rng(9), idx_mpc=77, seed=0,
                                 with_beta_cem=(cost == "mmd_opt"))
-    nat.begin(cost, 77, DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, xo, yo, 15.0, draws)
-    st = ora.init_state(DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, draws)
+    nat.begin(cost, 77, init, DEFAULT_MEAN, DEFAULT_COV, xo, yo, 15.0, draws)
+    st = ora.init_state(init, DEFAULT_MEAN, DEFAULT_COV, draws)
     _sync_state(nat, st, B)
     nat.run_stage(1, 0)
     pr, acc, steer = ora.front(st)

@@ -49,3 +49,24 @@ def test_batch_equals_sequential(cost, n, noise, variant):
     bat = run_block_batch(prob, hb, cost, ids, init, mean, cov, variant=variant)
     hb.close()
     assert np.array_equal(seq, bat), np.argwhere(seq != bat)[:5]
+
+
+def test_batch_two_groups_equals_sequential():
+    """A batch of 12 configurations x num_batch 100 (1200 candidates) runs its
+    beta-CEM as two candidate groups on two streams, the group boundary
+    inside a configuration (mpcmmd.hip: run_beta_cem) -- the production
+    path of `optimizer.sweep --batch 32`: rows bit-identical to one
+    configuration at a time."""
+    from optimizer import _native
+    from optimizer.cem import CEM
+    from optimizer.sweep import run_block, run_block_batch
+    prob = CEM(6, 3, 0.1, 12, "gaussian", 0.0, 0.0, num_batch=100, device=0, maxiter_cem=4)
+    init = np.array([0.0, 1.75, 5.0, 0.0, 0.0, 0.0], np.float32)
+    mean = np.array([15.0] * 4 + [0.0] * 4, np.float32)
+    cov = np.diag([20.0] * 4 + [100.0] * 4).astype(np.float32)
+    ids = range(12)
+    seq = run_block(prob, "mmd_opt", ids, init, mean, cov)
+    hb = _native.Handle(prob._cfg, max_configs=12)
+    bat = run_block_batch(prob, hb, "mmd_opt", ids, init, mean, cov)
+    hb.close()
+    assert np.array_equal(seq, bat), np.argwhere(seq != bat)[:5]
