@@ -83,48 +83,77 @@ struct ReduceScratch {
   int i[16];
   int list_n;
   float v_lo, v_hi;
+  unsigned long long t0;
+  unsigned long long gm[128];  // 8-lane group maxima of block_cvar (blockDim <= 1024)
 };
 
+// largest 64-bit word over each group of 8 lanes (quad butterflies, then
+// row_half_mirror pairs the two quads), in every lane of the group
+DEVI unsigned long long max8_u64(unsigned long long v) {
+  auto step = [](unsigned long long a, auto dpp) {
+    const unsigned long long b = (static_cast<unsigned long long>(unsigned(dpp(int(a >> 32)))) << 32) |
+                                 unsigned(dpp(int(a)));
+    return b > a ? b : a;
+  };
+  v = step(v, [](int x) { return dpp_i<0xB1>(x); });
+  v = step(v, [](int x) { return dpp_i<0x4E>(x); });
+  return step(v, [](int x) { return dpp_i<0x141>(x); });
+}
+
 // jnp.quantile(x, 0.98) (linear, JAX fp32 weights) + mean of the tail
-// (costs.py:215-219) over vals[0..S).  list: >= S ints of LDS scratch.
-// Sorted order = the jnp.argsort total order (ties by index).
+// (costs.py:215-219) over vals[0..S).  list: >= S 64-bit words of LDS.
+// Sorted order = the jnp.argsort total order (ties by index): the words
+// (sort key << 32 | index) are distinct and their unsigned order is it.
+// Ascending positions lo <= hi lie among the top need = S - lo words, so
+// only a window of the largest words is ranked: T0 = the need-th largest of
+// the 8-lane group maxima (each of those need groups holds a word >= T0, so
+// at least need words are >= T0, and at most need groups contribute), the
+// words >= T0 are compacted into LDS and ranked exactly among themselves.
 DEVI float block_cvar(const float* vals, int S, unsigned long long* list, ReduceScratch& rs) {
   const float pos = 0.98f * float(S - 1);
   const float flo = floorf(pos), fhi = ceilf(pos);
   const float hw = pos - flo;
   const float lw = 1.0f - hw;
   const int lo = min(max(int(flo), 0), S - 1), hi = min(max(int(fhi), 0), S - 1);
-  if (threadIdx.x == 0) rs.list_n = 0;
-  __syncthreads();
-  // zero class (key of +-0) sorts first: count it, compact the rest as
-  // (sort key, index) pairs -- their 64-bit order is the stable argsort's
-  int nz = 0;
-  for (int s = threadIdx.x; s < S; s += blockDim.x) {
-    const uint32_t k = sort_key(vals[s]);
-    if (k == 0x80000000u) {
-      ++nz;
-    } else {
-      const int slot = atomicAdd(&rs.list_n, 1);
-      list[slot] = (static_cast<unsigned long long>(k) << 32) | static_cast<unsigned>(s);
-    }
+  const int need = S - lo, tid = threadIdx.x, G = blockDim.x >> 3;
+  auto word = [&](int s) {
+    return (static_cast<unsigned long long>(sort_key(vals[s])) << 32) | static_cast<unsigned>(s);
+  };
+  unsigned long long km = 0;  // below every word (sort keys are >= 0x007FFFFF)
+  for (int s = tid; s < S; s += blockDim.x) {
+    const unsigned long long k = word(s);
+    km = k > km ? k : km;
   }
-  const int z = block_sum(nz, rs.i);  // also a barrier
-  const int m = rs.list_n;
-  if (threadIdx.x == 0) {
+  km = max8_u64(km);
+  if (tid == 0) {
+    rs.list_n = 0;
+    rs.t0 = 0;  // need > G: every word is in the window
     rs.v_lo = 0.0f;
     rs.v_hi = 0.0f;
   }
+  if ((tid & 7) == 0) rs.gm[tid >> 3] = km;
   __syncthreads();
-  if (hi >= z) {
-    for (int a = threadIdx.x; a < m; a += blockDim.x) {
-      const unsigned long long ka = list[a];
-      int r = 0;
-#pragma unroll 8
-      for (int c = 0; c < m; ++c) r += list[c] < ka;  // LDS broadcast reads
-      const int ia = int(ka & 0xFFFFFFFFull);
-      if (r == lo - z) rs.v_lo = vals[ia];
-      if (r == hi - z) rs.v_hi = vals[ia];
-    }
+  if (need <= G && tid < G) {
+    const unsigned long long g = rs.gm[tid];
+    int r = 0;
+    for (int q = 0; q < G; ++q) r += rs.gm[q] > g;  // LDS broadcast reads
+    if (r == need - 1) rs.t0 = g;  // empty groups (0) share a rank: any of them writes 0
+  }
+  __syncthreads();
+  const unsigned long long T0 = rs.t0;
+  for (int s = tid; s < S; s += blockDim.x) {
+    const unsigned long long k = word(s);
+    if (k >= T0) list[atomicAdd(&rs.list_n, 1)] = k;
+  }
+  __syncthreads();
+  const int c = rs.list_n;
+  for (int a = tid; a < c; a += blockDim.x) {
+    const unsigned long long ka = list[a];
+    int r = 0;  // words above ka: its position from the top
+    for (int q = 0; q < c; ++q) r += list[q] > ka;
+    const int ia = int(ka & 0xFFFFFFFFull);
+    if (r == S - 1 - lo) rs.v_lo = vals[ia];
+    if (r == S - 1 - hi) rs.v_hi = vals[ia];
   }
   __syncthreads();
   const float var = rs.v_lo * lw + rs.v_hi * hw;

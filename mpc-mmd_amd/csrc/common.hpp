@@ -21,22 +21,65 @@ namespace mpcmmd {
 
 constexpr int kWave = 64;
 
-// ---- wave-wide reductions (result valid in every lane) ----------------------
-DEVI double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-  return v;
+// ---- DPP helpers (gfx9 DPP controls) -----------------------------------------
+// quad_perm(1,0,3,2) 0xB1, quad_perm(2,3,0,1) 0x4E, row_ror:4 0x124,
+// row_ror:8 0x128, row_bcast:15 0x142, row_bcast:31 0x143.  Rows disabled by
+// ROWS read 0.
+template <int CTRL, int ROWS = 0xF>
+DEVI int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, false);
 }
-DEVI float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-  return v;
+template <int CTRL, int ROWS = 0xF>
+DEVI double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, int(b), CTRL, ROWS, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), CTRL, ROWS, 0xF, false);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
 }
-DEVI int wave_sum(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-  return v;
+DEVI float readlane_f(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
+DEVI double readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane(int(b), l);
+  const int hi = __builtin_amdgcn_readlane(int(b >> 32), l);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+
+// ---- wave-wide reductions (wave-uniform result) --------------------------------
+// Sums: quad and row butterflies by DPP, then the row broadcasts into lane 63
+// and one readlane -- VALU only (a __shfl_xor butterfly is six LDS-crossbar
+// round trips, ds_bpermute, per sum).
+DEVI int wave_total(int v) {
+  v += dpp_i<0xB1>(v);
+  v += dpp_i<0x4E>(v);
+  v += dpp_i<0x124>(v);
+  v += dpp_i<0x128>(v);
+  v += dpp_i<0x142, 0xA>(v);
+  v += dpp_i<0x143, 0xC>(v);
+  return __builtin_amdgcn_readlane(v, 63);
+}
+DEVI float wave_total(float v) {
+  v += __int_as_float(dpp_i<0xB1>(__float_as_int(v)));
+  v += __int_as_float(dpp_i<0x4E>(__float_as_int(v)));
+  v += __int_as_float(dpp_i<0x124>(__float_as_int(v)));
+  v += __int_as_float(dpp_i<0x128>(__float_as_int(v)));
+  v += __int_as_float(dpp_i<0x142, 0xA>(__float_as_int(v)));
+  v += __int_as_float(dpp_i<0x143, 0xC>(__float_as_int(v)));
+  return readlane_f(v, 63);
+}
+DEVI double wave_total(double v) {
+  v += dpp_d<0xB1>(v);
+  v += dpp_d<0x4E>(v);
+  v += dpp_d<0x124>(v);
+  v += dpp_d<0x128>(v);
+  v += dpp_d<0x142, 0xA>(v);
+  v += dpp_d<0x143, 0xC>(v);
+  return readlane_d(v, 63);
+}
+DEVI double wave_sum(double v) { return wave_total(v); }
+DEVI float wave_sum(float v) { return wave_total(v); }
+DEVI int wave_sum(int v) { return wave_total(v); }
 DEVI float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
@@ -59,9 +102,6 @@ DEVI unsigned long long wave_min_u64(unsigned long long v) {
   return v;
 }
 
-DEVI float readlane_f(float v, int lane) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
-}
 
 // ---- ordering ----------------------------------------------------------------
 // jnp.argsort total order on fp32: -0 == +0, every NaN equal and last.

@@ -63,20 +63,6 @@ DEVI void wave_sync() {
   __asm__ volatile("" ::: "memory");
 }
 
-// ---- DPP helpers (gfx9 DPP controls) ------------------------------------
-// quad_perm(1,0,3,2) 0xB1, quad_perm(2,3,0,1) 0x4E, row_ror:4 0x124,
-// row_ror:8 0x128, row_bcast:15 0x142, row_bcast:31 0x143
-template <int CTRL, int ROWS = 0xF>
-DEVI int dpp_i(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, false);
-}
-template <int CTRL, int ROWS = 0xF>
-DEVI double dpp_d(double v) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, int(b), CTRL, ROWS, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), CTRL, ROWS, 0xF, false);
-  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
-}
 // v_permlane32_swap (W = 32): lanes 32-63 of x <-> lanes 0-31 of y;
 // v_permlane16_swap (W = 16): the odd 16-lane rows of x <-> the even rows of y.
 // Inline asm: hipcc (ROCm 7.2) may commute the builtins' two operands, which
@@ -89,32 +75,6 @@ DEVI void permlane_swap(float& x, float& y) {
     __asm__ volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
 }
 
-// sum of the 64 lanes, wave-uniform result (VALU only: quad / row butterflies,
-// then the row broadcasts into lane 63)
-DEVI int wave_total(int v) {
-  v += dpp_i<0xB1>(v);
-  v += dpp_i<0x4E>(v);
-  v += dpp_i<0x124>(v);
-  v += dpp_i<0x128>(v);
-  v += dpp_i<0x142, 0xA>(v);
-  v += dpp_i<0x143, 0xC>(v);
-  return __builtin_amdgcn_readlane(v, 63);
-}
-DEVI double readlane_d(double v, int l) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane(int(b), l);
-  const int hi = __builtin_amdgcn_readlane(int(b >> 32), l);
-  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
-}
-DEVI double wave_total(double v) {
-  v += dpp_d<0xB1>(v);
-  v += dpp_d<0x4E>(v);
-  v += dpp_d<0x124>(v);
-  v += dpp_d<0x128>(v);
-  v += dpp_d<0x142, 0xA>(v);
-  v += dpp_d<0x143, 0xC>(v);
-  return readlane_d(v, 63);
-}
 // sum over each row of 16 lanes (every lane of the row holds it)
 DEVI double row16_sum(double v) {
   v += dpp_d<0xB1>(v);
@@ -504,10 +464,22 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int kSampleTiles = kBzCols / 16;  // 6 tiles of 16 sample columns (89 used)
 static_assert(kBzCols >= kNew, "sample tiles");
 // TPW = sample tiles per wave: 6 (one wave per candidate: the generator
-// operands loaded once) when the batch fills the chip, else 2 or 1 (3 or 6
-// waves per candidate, each loading the block's generators itself) so a
-// small batch -- the reference's num_batch = 100 -- still spreads over the
-// SIMDs
+// operands loaded once) when the batch fills the chip; small batches -- the
+// reference's num_batch = 100 -- take k_bsample_chunks (one tile per wave,
+// the blocks split into chunks walked in parallel).
+//
+// The prefix is kept as S = S_pre + S_loc: S_loc accumulates W^T Z from zero
+// within a chunk of sample_chunk(nblk) blocks and is folded into S_pre at the
+// chunk's end.  The chunking depends only on M, so one wave walking every
+// chunk (k_bsample) and one wave per chunk (k_bsample_chunks, S_pre from the
+// earlier chunks' sums) compute the same bits: a configuration's samples do
+// not depend on the batch it is solved in.
+constexpr int kChunkWavesMax = 12;
+HDI int sample_chunk(int nblk) {
+  int cl = 8;
+  while ((nblk + cl - 1) / cl > kChunkWavesMax) cl <<= 1;
+  return cl;
+}
 template <int TPW>
 constexpr int sample_waves() {
   static_assert(kSampleTiles % TPW == 0, "tiles per wave");
@@ -571,15 +543,21 @@ DEVI void load_block(SampleBlock<TPW>& q, const double* G, const double* gm, con
 // dependent steps.  No VALU work on the accumulators: the pipe never waits
 // for a vector add between blocks.
 template <int TPW>
-DEVI void block_mfma(const SampleBlock<TPW>& cur, d4* S, d4* Y, int r, int h) {
+DEVI void block_mfma(const SampleBlock<TPW>& cur, d4* S, const d4* Sp, d4* Y, int r, int h) {
   d4 X = d4{0.0, 0.0, 0.0, 0.0};  // X = W_c U_c^T: register i holds w_{h+4i} . u_r = T[row r][col h + 4i]
 #pragma unroll
   for (int i = 0; i < 3; ++i) X = mfma64(cur.wX[i], cur.uX[i], X);
   const d4 m = d4{cur.m[0], cur.m[1], cur.m[2], cur.m[3]};
+  // B operand of U S: S_pre + S_loc (rows 0..11 of S: registers 0..2)
+  double St[TPW][3];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) St[t][k] = Sp[t][k] + S[t][k];
 #pragma unroll
   for (int k = 0; k < 3; ++k)
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) Y[t] = mfma64(cur.uX[k], S[t][k], k == 0 ? m : Y[t]);
+    for (int t = 0; t < TPW; ++t) Y[t] = mfma64(cur.uX[k], St[t][k], k == 0 ? m : Y[t]);
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
@@ -618,6 +596,13 @@ DEVI void block_store(const d4* Yv, float* Y, int p0, int M, int ys, int h) {
   }
 }
 
+// S_pre += S_loc, S_loc = 0 (a chunk's end)
+DEVI void fold_chunk(d4& Sp, d4& S) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) Sp[k] = Sp[k] + S[k];
+  S = d4{0.0, 0.0, 0.0, 0.0};
+}
+
 template <int TPW>
 __global__ __launch_bounds__(64 * sample_waves<TPW>()) void k_bsample(Params p, int tb) {
   const int b = p.b0 + blockIdx.x, M = p.M, Pp = pos_pad(M);
@@ -630,32 +615,105 @@ __global__ __launch_bounds__(64 * sample_waves<TPW>()) void k_bsample(Params p, 
   const double* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
   const int ys = ygen_stride(M);
   float* Y = p.ygen + (size_t(b) * kBzCols + s0 + (TPW == 1 ? r : 2 * r)) * ys;
-  d4 S[TPW], Ya[TPW], Yb[TPW];
+  d4 S[TPW], Sp[TPW], Ya[TPW], Yb[TPW];
 #pragma unroll
-  for (int t = 0; t < TPW; ++t) S[t] = d4{0.0, 0.0, 0.0, 0.0};
-  const int nblk = Pp >> 4;
+  for (int t = 0; t < TPW; ++t) S[t] = Sp[t] = d4{0.0, 0.0, 0.0, 0.0};
+  const int nblk = Pp >> 4, cl = sample_chunk(nblk);
   // blocks in pairs, operands and outputs ping-ponged: the next block's loads
   // are in flight and its MFMAs issued while the previous block's samples
-  // are converted and stored (the last prefetch re-reads a block; nblk is
-  // even; sched barriers keep that order)
+  // are converted and stored (the last prefetch re-reads a block; nblk and
+  // the chunk length are even; sched barriers keep that order)
   SampleBlock<TPW> qa, qb;
   load_block(qa, G, gm, z, 0, s0, r, h);
   for (int c = 0; c < nblk; c += 2) {
     const int p0 = c << 4;
     load_block(qb, G, gm, z, p0 + 16, s0, r, h);
     __builtin_amdgcn_sched_barrier(0);
-    block_mfma(qa, S, Ya, r, h);
+    block_mfma(qa, S, Sp, Ya, r, h);
     __builtin_amdgcn_sched_barrier(0);
     if (c > 0) block_store<TPW>(Yb, Y, p0 - 16, M, ys, h);
     __builtin_amdgcn_sched_barrier(0);
     load_block(qa, G, gm, z, min(p0 + 32, Pp - 16), s0, r, h);
     __builtin_amdgcn_sched_barrier(0);
-    block_mfma(qb, S, Yb, r, h);
+    block_mfma(qb, S, Sp, Yb, r, h);
+    if ((c + 2) % cl == 0)
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) fold_chunk(Sp[t], S[t]);
     __builtin_amdgcn_sched_barrier(0);
     block_store<TPW>(Ya, Y, p0, M, ys, h);
     __builtin_amdgcn_sched_barrier(0);
   }
   block_store<TPW>(Yb, Y, Pp - 16, M, ys, h);
+  MPCMMD_STAMP(p, 1);
+}
+
+// k_bsample_chunks: the samples of k_bsample for small batches, workgroup =
+// (candidate, tile of 16 samples), one wave per chunk of blocks.  Phase 1:
+// each wave but the last sums W^T Z over its chunk (the MFMAs of the walker's
+// S_loc, from zero) into LDS; phase 2: S_pre = the earlier chunks' sums in
+// order (the walker's folds), then the chunk's blocks as in k_bsample.
+__global__ __launch_bounds__(64 * kChunkWavesMax) void k_bsample_chunks(Params p, int tb) {
+  __shared__ double dS[kChunkWavesMax - 1][3][64];
+  const int b = p.b0 + blockIdx.x, M = p.M, Pp = pos_pad(M), nblk = Pp >> 4;
+  const int lane = threadIdx.x & 63, k = threadIdx.x >> 6, P = blockDim.x >> 6;
+  const int r = lane & 15, h = lane >> 4, s0 = blockIdx.y * 16;
+  const int cl = sample_chunk(nblk), c0 = k * cl, c1 = min(nblk, c0 + cl);
+  MPCMMD_STAMP(p, 0);
+  const double* G = p.gen + size_t(b) * Pp * kGenStride;
+  const double* gm = p.genm + size_t(b) * Pp;
+  const double* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
+  const int ys = ygen_stride(M);
+  float* Y = p.ygen + (size_t(b) * kBzCols + s0 + r) * ys;
+  if (k < P - 1) {
+    // operands of W^T Z for block c: W[p0 + 4 kk + h][r], Z[p0 + 4 kk + h][s0 + r]
+    auto ld = [&](double (&wa)[4], double (&zz)[4], int c) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const size_t pos = size_t(c) * 16 + 4 * kk + h;
+        wa[kk] = G[pos * kGenStride + kGenW + r];
+        zz[kk] = z[pos * kBzCols + s0 + r];
+      }
+    };
+    d4 Sl = d4{0.0, 0.0, 0.0, 0.0};
+    double wa[4], zz[4], wn[4], zn[4];
+    ld(wa, zz, c0);
+    for (int c = c0; c < c1; ++c) {
+      ld(wn, zn, min(c + 1, c1 - 1));
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) Sl = mfma64(wa[kk], zz[kk], Sl);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        wa[kk] = wn[kk];
+        zz[kk] = zn[kk];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) dS[k][i][lane] = Sl[i];
+  }
+  __syncthreads();
+  d4 S[1] = {d4{0.0, 0.0, 0.0, 0.0}}, Sp[1] = {d4{0.0, 0.0, 0.0, 0.0}}, Ya[1], Yb[1];
+  for (int j = 0; j < k; ++j)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) Sp[0][i] = Sp[0][i] + dS[j][i][lane];
+  SampleBlock<1> qa, qb;
+  const int pend = c1 << 4;
+  load_block(qa, G, gm, z, c0 << 4, s0, r, h);
+  for (int c = c0; c < c1; c += 2) {
+    const int p0 = c << 4;
+    load_block(qb, G, gm, z, p0 + 16, s0, r, h);
+    __builtin_amdgcn_sched_barrier(0);
+    block_mfma(qa, S, Sp, Ya, r, h);
+    __builtin_amdgcn_sched_barrier(0);
+    if (c > c0) block_store<1>(Yb, Y, p0 - 16, M, ys, h);
+    __builtin_amdgcn_sched_barrier(0);
+    load_block(qa, G, gm, z, min(p0 + 32, pend - 16), s0, r, h);
+    __builtin_amdgcn_sched_barrier(0);
+    block_mfma(qb, S, Sp, Yb, r, h);
+    __builtin_amdgcn_sched_barrier(0);
+    block_store<1>(Ya, Y, p0, M, ys, h);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  block_store<1>(Yb, Y, pend - 16, M, ys, h);
   MPCMMD_STAMP(p, 1);
 }
 
@@ -1260,18 +1318,6 @@ __global__ __launch_bounds__(qp_threads(NP), NP == 24 ? 3 : (NP <= 16 ? 4 : 2)) 
 // one backward solve (column sums as wave reductions).  fp32 like the quad
 // kernel; the cost beta^T K beta - 2 g^T beta in fp64 on the fp32 beta with
 // K_red re-read.
-DEVI float readlane_f(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
-DEVI float wave_total(float v) {
-  int b = __float_as_int(v);
-  v += __int_as_float(dpp_i<0xB1>(b));
-  v += __int_as_float(dpp_i<0x4E>(__float_as_int(v)));
-  v += __int_as_float(dpp_i<0x124>(__float_as_int(v)));
-  v += __int_as_float(dpp_i<0x128>(__float_as_int(v)));
-  v += __int_as_float(dpp_i<0x142, 0xA>(__float_as_int(v)));
-  v += __int_as_float(dpp_i<0x143, 0xC>(__float_as_int(v)));
-  return readlane_f(v, 63);
-}
-
 template <int NP>
 __global__ __launch_bounds__(256) void k_bqp_wave(Params p, int tb) {
   const int lane = threadIdx.x & 63;
@@ -1795,14 +1841,13 @@ void launch_bdist(const Params& p, hipStream_t s) {
 
 void launch_bsample(const Params& p, int tb, hipStream_t s) {
   // one wave per candidate when the launch alone holds >= ~half a wave per
-  // SIMD; smaller batches split the sample tiles over 3 waves (num_batch =
-  // 100: 7.9 -> 3.9 ms per step) or, below 60 candidates, 6
-  if (p.nb >= 384)
+  // SIMD; smaller batches one wave per (candidate, tile, chunk)
+  if (p.nb >= 384) {
     hipLaunchKernelGGL((k_bsample<6>), dim3(p.nb), dim3(64 * sample_waves<6>()), 0, s, p, tb);
-  else if (p.nb >= 60)
-    hipLaunchKernelGGL((k_bsample<2>), dim3(p.nb), dim3(64 * sample_waves<2>()), 0, s, p, tb);
-  else
-    hipLaunchKernelGGL((k_bsample<1>), dim3(p.nb), dim3(64 * sample_waves<1>()), 0, s, p, tb);
+  } else {
+    const int nblk = pos_pad(p.M) >> 4, cl = sample_chunk(nblk);
+    hipLaunchKernelGGL(k_bsample_chunks, dim3(p.nb, kSampleTiles), dim3(64 * ((nblk + cl - 1) / cl)), 0, s, p, tb);
+  }
 }
 
 // waves per candidate: ~16 single-wave workgroups per SIMD over the launch,
