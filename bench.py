@@ -78,9 +78,11 @@ HBM_PEAK_GBS = 8000.0
 def kernel_work(w, name, launches, stats):
     """Algorithmic work of the profiled launches of kernel `name` (DESIGN.md
     §4): (bound, unit, amount, peak).
-      bkernel  (sample, row) pairs summed (counted by the kernel, stats[1])
-               x (M exp terms + (n-1)/2 K_red entries), against the exp-term
-               issue floor (EXP_TERM_PEAK)
+      bkernel  series row sums and K_red: its HBM bytes (K_red entries
+               written, 4 B each (stats[3]); per series pair (stats[2]) the
+               4-B selection read and the 4-B row sum written) against HBM
+      bdirect  directly summed (sample, row) pairs (stats[1]) x M exp terms,
+               against the exp-term issue floor (EXP_TERM_PEAK)
       bsample  per candidate and beta-iteration, per 16-position block and 89
                samples: T Z 16x16, U S 16x11, W^T Z 11x16 (2 flop each) +
                W U^T 16x16x11, on fp64 MFMA
@@ -94,7 +96,9 @@ def kernel_work(w, name, launches, stats):
     n = w["num_reduced"]
     M = n * n
     if name == "bkernel":
-        return "exp-issue", "T exp-terms/s", stats[1] * (M + (n - 1) / 2), EXP_TERM_PEAK
+        return "hbm", "GB/s", stats[3] * 4 + stats[2] * 8, HBM_PEAK_GBS, 1e9
+    if name == "bdirect":
+        return "exp-issue", "T exp-terms/s", stats[1] * M, EXP_TERM_PEAK
     if name == "bsample":
         nblk = (((M + 1) + 31) // 32) * 2
         per = nblk * 89 * 2 * (16 * 16 + 16 * 11 + 11 * 16) + nblk * 16 * 16 * 11 * 2
@@ -257,12 +261,16 @@ def run_workload(name, steps, warmup, profile_steps, rank, world, local, dist=No
     roof = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None}
     model = kernel_work(w, dom, launches, stats)
     if model is not None:
-        bound, unit, amount, peak = model
-        roof.update(bound=bound, unit=unit, peak=peak, achieved=amount / launches / avg_s / 1e12)
+        bound, unit, amount, peak = model[:4]
+        scale = model[4] if len(model) > 4 else 1e12  # unit of `achieved` (T/s; GB/s for HBM bounds)
+        roof.update(bound=bound, unit=unit, peak=peak, achieved=amount / launches / avg_s / scale)
         roof["frac"] = roof["achieved"] / peak
     roof["traffic"] = pmc_traffic(name, dom)
     roof["kernel"] = dom
     roof["avg_us"] = avg_s * 1e6
+    if w["cost"] == "mmd_opt":  # k_bkernel work counters over the profiled pass
+        roof["bkernel_counts"] = {"direct_rows": int(stats[0]), "direct_pairs": int(stats[1]),
+                                  "series_pairs": int(stats[2]), "kred_entries": int(stats[3])}
     return dict(w=w, elapsed=elapsed, step_ms=step_ms, res=res, roof=roof, inst=inst,
                 kernels={k: v[1] / profile_steps for k, v in busy.items()})
 

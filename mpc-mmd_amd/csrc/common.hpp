@@ -19,6 +19,14 @@ namespace mpcmmd {
   } while (0)
 
 
+// per-workgroup phase timestamp into dbgw[blockIdx.x][slot] (profiling only;
+// the workgroups of one launch, slots 0..7)
+#define MPCMMD_STAMPW(p, slot)                                                  \
+  do {                                                                          \
+    if (threadIdx.x == 0 && (p).dbgw && blockIdx.x < 65536)                     \
+      (p).dbgw[size_t(blockIdx.x) * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
 constexpr int kWave = 64;
 
 // ---- DPP helpers (gfx9 DPP controls) -----------------------------------------

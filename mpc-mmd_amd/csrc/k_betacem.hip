@@ -22,7 +22,7 @@
 // kernels of different groups (bound by different units: MFMA, exp, fp64
 // FMA latency, LDS) run side by side.  Every supported size n <= 64
 // (M = n^2 <= 4096) takes the same kernels; the LDS-resident pieces are sized
-// at launch (ker_lds, elite_lds).
+// at launch (ker_lds, dir_lds, elite_lds).
 //
 // The covariance of the beta-CEM is rank <= 10 plus 0.05 I
 // (jnp.cov of 11 elites, compute_beta.py:61).  Its Cholesky factor is never
@@ -122,11 +122,18 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
       if (h == H - 1) break;
       bicycle_step(x, y, vx, vy, psi, ar[h], sr[h]);
     }
+    float fr[kFeatStride];
 #pragma unroll
     for (int k = 0; k < 11; ++k) {
-      F[k * M + m] = float(cx[k]);
-      F[(11 + k) * M + m] = float(cy[k]);
+      fr[k] = float(cx[k]);
+      fr[11 + k] = float(cy[k]);
+      F[k * M + m] = fr[k];
+      F[(11 + k) * M + m] = fr[11 + k];
     }
+    fr[22] = fr[23] = 0.0f;
+    float4* Fr = reinterpret_cast<float4*>(p.featr + (size_t(b) * M + m) * kFeatStride);
+#pragma unroll
+    for (int q = 0; q < kFeatStride / 4; ++q) Fr[q] = make_float4(fr[4 * q], fr[4 * q + 1], fr[4 * q + 2], fr[4 * q + 3]);
   }
 }
 
@@ -210,6 +217,77 @@ __global__ __launch_bounds__(kDistThreads) void k_bdist(Params p) {
     }
     __syncthreads();
   }
+}
+
+// ------------------------------------------------------------------------
+// k_bmoment: the series record of every distance row (once per outer
+// iteration, after k_bdist).  A K_mixed row sum of sample s over the mother
+// set (kernel_computation.py:33-39, 45; compute_beta.py:75) is
+//   S(r, c) = sum_j exp(-c D[r][j]),  c = 1 / sigma_s.
+// With R = max_j D[r][j] / 2, t_j = D[r][j] / R - 1 in [-1, 1] and a = c R,
+//   S = exp(-a) sum_j exp(-a t_j) = exp(-a) sum_{k < 12} (-a)^k / k! P_k + E,
+//   P_k = sum_j t_j^k,   |E| / S <= e^{2a} a^12 / 12!
+// (each term's Taylor remainder is <= a^12 e^a / 12! while each term is
+// >= e^-a), i.e. <= 1.5e-8 for a <= 1: below half an fp32 ulp, so the
+// series is as exact as the reference's fp32 exponentials and sum.  P_k
+// depends on the row only; k_bkernel then pays a 12-term Horner sum per
+// (sample, row) pair instead of M exponentials (pairs with a > 1 are summed
+// directly).  One wave per row: the row as float4s in registers, the row max
+// by DPP, t and its powers in packed fp32 (the column pairs of a float4 as
+// one v_pk_* operand), one wave sum per moment.  Pad columns (+inf) count 0.
+constexpr int kMomRowsPerBlock = 4;
+
+template <int NV4>
+__global__ __launch_bounds__(64 * kMomRowsPerBlock) void k_bmoment(Params p) {
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * kMomRowsPerBlock + (threadIdx.x >> 6);
+  const int M = p.M, Md = dist_stride(M);
+  if (gw >= p.Bt * M) return;  // wave-uniform
+  const int b = gw / M, r = gw - b * M;
+  const float4* row = reinterpret_cast<const float4*>(p.bdist + (size_t(b) * M + r) * Md) + lane;
+  float4 x[NV4];
+#pragma unroll
+  for (int t = 0; t < NV4; ++t) x[t] = row[64 * t];
+  // columns j = 4 (lane + 64 t) + c; pad columns j >= M
+  auto valid = [&](int t, int c) { return 4 * (lane + 64 * t) + c < M; };
+  float mx = 0.0f;
+#pragma unroll
+  for (int t = 0; t < NV4; ++t) {
+    if (valid(t, 0)) mx = fmaxf(mx, x[t].x);
+    if (valid(t, 1)) mx = fmaxf(mx, x[t].y);
+    if (valid(t, 2)) mx = fmaxf(mx, x[t].z);
+    if (valid(t, 3)) mx = fmaxf(mx, x[t].w);
+  }
+  const float R = 0.5f * wave_max(mx);
+  const float invR = R > 0.0f ? 1.0f / R : 0.0f;  // R = 0: every t = -1, every a = 0
+  f2 acc[kMom - 1];
+#pragma unroll
+  for (int k = 0; k < kMom - 1; ++k) acc[k] = f2{0.0f, 0.0f};
+#pragma unroll
+  for (int t = 0; t < NV4; ++t) {
+    const float e[4] = {x[t].x, x[t].y, x[t].z, x[t].w};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float t0 = valid(t, 2 * h) ? fmaf(e[2 * h], invR, -1.0f) : 0.0f;
+      const float t1 = valid(t, 2 * h + 1) ? fmaf(e[2 * h + 1], invR, -1.0f) : 0.0f;
+      const f2 tt = {t0, t1};
+      f2 pw = tt;
+#pragma unroll
+      for (int k = 0; k < kMom - 1; ++k) {
+        acc[k] += pw;
+        if (k + 1 < kMom - 1) pw *= tt;
+      }
+    }
+  }
+  float rec = 0.0f;  // lane k < 16 ends up holding slot k of the record
+#pragma unroll
+  for (int k = 0; k < kMom - 1; ++k) {
+    const float s = wave_total(acc[k].x + acc[k].y);
+    if (lane == k + 1) rec = s;
+  }
+  if (lane == 0) rec = float(M);
+  if (lane == kMomR) rec = R;
+  if (lane < kMomStride) p.bmom[(size_t(b) * M + r) * kMomStride + lane] = rec;
 }
 
 // ------------------------------------------------------------------------
@@ -755,75 +833,116 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
 }
 
 // ------------------------------------------------------------------------
-// k_bkernel: kernel_computation.py:19-65 / compute_beta.py:120-127 for every
-// sample of the iteration.  Workgroup = (candidate, part); a candidate's
-// distinct rows are split over `split` parts when the batch alone cannot
-// fill the chip.
+// k_bkernel + k_bdirect: kernel_computation.py:19-65 / compute_beta.py:120-127
+// for every sample of the iteration: the K_mixed row sums and K_red.
 //
-//   pairs    (sample s, reduced position k) of this iteration's selections,
-//            counting-sorted by their mother row r = sel[s][k] (LDS), and
-//            the list of the distinct rows (~150 of 484 at n = 22)
-//   rows     a wave takes the next distinct row (LDS counter) and holds its
-//            distance-matrix row (k_bdist, kernel_computation.py:33-39) in
-//            registers (lane L: float4s L + 64 t); for small rows the next
-//            row's loads are issued before the current one is summed.  The
-//            row's pairs are summed 8 at a time: per lane and pair the
-//            lane's terms exp2(D[r][j] * (-log2 e / sigma_s)) (v_exp_f32,
-//            packed scale / add), then one transposing cross-lane reduction
-//            (permlane32 / permlane16 swaps, DPP) leaves pair j's row sum in
-//            lane 8 j + 4
-//   K_red    the batch's entries exp(-D[r][sel[s][kk]] / sigma_s), kk < k
-//            (8 lanes per pair), gathered from a wave-private LDS copy of the row
-// No D row is staged through a shared buffer, so there are no barriers after
-// the setup and no chunk quantisation: every exp is one of the M terms of a
-// real pair (plus the row padding to whole 256-column blocks).
+// k_bkernel, workgroup = (candidate, part of its samples):
+//   union    the distinct mother rows the iteration's samples select (LDS
+//            flags, scan): their rank and their series records (k_bmoment),
+//            staged in LDS
+//   series   every (sample s, reduced position k) pair whose a = R_r / sigma_s
+//            is <= 1: row sum = exp(-a) * a 12-term Horner sum over the row's
+//            moments, fp64, one thread per pair; the other pairs are flagged
+//            for k_bdirect (Params::bdflag, a count per part in bdcount)
+//   K_red    exp(-D[sel_k][sel_kk] / sigma_s), kk < k, the distances
+//            recomputed from the feature rows (Params::featr) in k_bdist's
+//            sequential feature order (bit-equal to D's entries), consecutive
+//            entries stored by consecutive lanes.  When the pairwise distances
+//            of the union fit the LDS budget (after the first few
+//            beta-iterations the samples concentrate: ~40-150 distinct rows
+//            of 484 at n = 22) they are computed once (a lane per row a, the
+//            rows b < a as LDS broadcasts) and each sample's entries are
+//            exponentials of table lookups (a wave per sample, the lookups of
+//            all its entries in flight together); otherwise a wave per sample
+//            stages its n feature rows in LDS and forms its n (n - 1) / 2
+//            distances, one lane per entry.
+// k_bdirect, workgroup = (candidate, part of its rows), only when a candidate
+// has flagged pairs (a > 1: mostly the first beta-iteration, whose samples
+// clipped to sigma = 0.01 have a ~ 100): the flagged pairs counting-sorted by
+// mother row r (LDS); a wave takes the next distinct row (LDS counter,
+// heaviest first) and holds its distance row (k_bdist) in registers (lane L:
+// float4s L + 64 t; for short rows the next row's loads are issued before the
+// current one is summed).  The row's pairs are summed 8 at a time: per lane
+// and pair the lane's terms exp2(D[r][j] * (-log2 e / sigma_s)) (v_exp_f32,
+// packed scale / add), then one transposing cross-lane reduction (permlane32
+// / permlane16 swaps, DPP) leaves pair j's row sum in lane 8 j + 4.
 // From the second beta-iteration on, samples 0..10 are the previous elites:
 // their selection, kernels and QP are unchanged, k_belite carried them, and
 // only samples 11..99 are processed here.
-constexpr int kKerWavesMax = 16;
+constexpr int kKerWaves = 16;
+constexpr int kDirWaves = 4;
+constexpr int kLptBins = 128;        // pair counts per distinct row (<= 100 samples)
+constexpr double kSeriesAMax = 1.0;  // k_bmoment's error bound holds for a <= 1
+constexpr size_t kLdsBudget = 160 * 1024 - 1024;
 
-constexpr int kLptBins = 128;  // pair counts per distinct row (<= 100 samples)
-
-struct KerLds {
-  size_t sel, csg, pairs, ulist, ustart, order, bins, misc, rowbuf, total;
-};
-
-// persistent: sel (short), csg, pairs (K_red offset | k << 18 | s << 24), the distinct rows
-// and their first pair; the setup's counts / fill / scan (10 M bytes) overlay
-// the wave row buffers.  Rows longer than kRowLdsMaxV4 float4s per lane are
-// not copied to LDS (the K_red gathers read the row from global memory, L2-hot
-// from the wave's own load): 16 waves per workgroup also at M = 2500.
-constexpr int kRowLdsMaxV4 = 4;
-HDI bool row_in_lds(int M) { return (dist_stride(M) >> 8) <= kRowLdsMaxV4; }
-HDI KerLds ker_lds(int M, int n, int waves) {
-  KerLds L{};
+struct LdsTake {  // consecutive 16-byte aligned LDS pieces
   size_t o = 0;
-  auto take = [&](size_t bytes) {
+  HDI size_t operator()(size_t bytes) {
     const size_t at = o;
     o = (o + bytes + 15) & ~size_t(15);
     return at;
-  };
+  }
+};
+
+// k_bkernel LDS.  persistent: sel (short; union ranks once the records are
+// staged), -log2 e / sigma, 1 / sigma, the entry table (k | kk << 8), union
+// rank of a row, row of a rank; scratch (`scratch` bytes, chosen at launch):
+// the union flags, then the union's series records, then the distance table
+// and the union's feature rows, or the waves' per-sample feature rows
+struct KerLds {
+  size_t sel, csg, csd, tri, urank, urow, misc, scratch, total;
+};
+HDI KerLds ker_lds(int M, int n, size_t scratch) {
+  KerLds L{};
+  LdsTake take;
   L.sel = take(size_t(kBetaSamples) * n * 2);
   L.csg = take(size_t(kBetaSamples) * 4);
-  L.pairs = take(size_t(kBetaSamples) * n * 4);
+  L.csd = take(size_t(kBetaSamples) * 8);
+  L.tri = take(size_t(n) * (n - 1));
+  L.urank = take(size_t(M) * 2);
+  L.urow = take(size_t(M) * 2);
+  L.misc = take(32 * 4);  // [0] union rows, [1] series pairs, [2] direct pairs, [16..] wave totals
+  L.scratch = take(scratch);
+  L.total = take.o;
+  return L;
+}
+HDI size_t ker_sample_bytes(int n) { return size_t(kKerWaves) * n * kFeatStride * 4; }
+HDI size_t ker_tab_bytes(int U) { return ((size_t(U) * (U - 1) / 2 * 4 + 15) & ~size_t(15)) + size_t(U) * kFeatStride * 4; }
+constexpr size_t kKerTabBytes = 55 * 1024;  // the table of a union of <= 144 rows
+// scratch: the series records of every mother row (up to kKerRecBytes;
+// larger unions read them from global memory), and the union table (up to
+// kKerTabBytes) from the second beta-iteration on (the first one's 100 fresh
+// samples select nearly every mother row)
+constexpr size_t kKerRecBytes = 64 * 1024;
+HDI size_t ker_scratch(int M, int n, int tb) {
+  size_t sc = ker_sample_bytes(n);
+  size_t rec = size_t(M) * kMomStride * 4;
+  if (rec > kKerRecBytes) rec = kKerRecBytes;
+  if (rec > sc) sc = rec;
+  if (tb > 0 && kKerTabBytes > sc) sc = kKerTabBytes;
+  return sc;
+}
+
+// k_bdirect LDS.  persistent: sel (short), -log2 e / sigma, the direct pairs
+// sorted by row, the distinct direct rows and their first pair, the grab
+// order; scratch: the setup's counts / fill / scan (10 M bytes)
+struct DirLds {
+  size_t sel, csg, pairs, ulist, ustart, order, bins, misc, scratch, total;
+};
+HDI DirLds dir_lds(int M, int n) {
+  DirLds L{};
+  LdsTake take;
+  L.sel = take(size_t(kBetaSamples) * n * 2);
+  L.csg = take(size_t(kBetaSamples) * 4);
+  L.pairs = take(size_t(kBetaSamples) * n * 2);
   L.ulist = take(size_t(M) * 2);
   L.ustart = take(size_t(M + 1) * 2);
   L.order = take(size_t(M) * 2);
   L.bins = take(kLptBins * 4);
-  L.misc = take(32 * 4);  // [0] next row, [1] distinct rows, [16..31] scan wave totals
-  const size_t rb = row_in_lds(M) ? size_t(waves) * dist_stride(M) * 4 : 0, setup = size_t(M) * 10;
-  L.rowbuf = take(rb > setup ? rb : setup);
-  L.total = o;
+  L.misc = take(32 * 4);  // [0] next row, [1] distinct rows, [16..] wave totals
+  L.scratch = take(size_t(M) * 10);
+  L.total = take.o;
   return L;
-}
-
-constexpr size_t kLdsBudget = 160 * 1024 - 1024;
-// waves per workgroup: 16 (one workgroup per candidate and half a CU) while
-// the row buffers leave room for two workgroups per CU
-int ker_waves(int M, int n) {
-  int wv = kKerWavesMax;
-  while (wv > 4 && ker_lds(M, n, wv).total > 80 * 1024) wv >>= 1;
-  return wv;
 }
 
 constexpr float kNegLog2e = -1.44269504088896340736f;
@@ -855,48 +974,291 @@ DEVI float transpose_sum8(const float (&v)[8]) {
   return x + __int_as_float(dpp_i<0x124>(__float_as_int(x)));
 }
 
-template <int NV4>
-__global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb, int split, int lpt) {
-  constexpr bool kPrefetch = NV4 <= 4;
+// 1 / (k + 1) for the Horner steps of the series
+__constant__ double kInvK[kMom] = {1.0,       1.0 / 2,  1.0 / 3,  1.0 / 4,  1.0 / 5,  1.0 / 6,
+                                   1.0 / 7,   1.0 / 8,  1.0 / 9,  1.0 / 10, 1.0 / 11, 1.0 / 12};
+
+// row sum of one pair by the series: q = the row's record, na = -a.  The
+// Horner sum in fp64; exp(-a) by v_exp_f32 (~1 ulp: the sum is rounded to
+// fp32 anyway, as the reference's fp32 terms are)
+DEVI float series_sum(const float4 (&q)[3], double na) {
+  const double P[kMom] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y,
+                          q[1].z, q[1].w, q[2].x, q[2].y, q[2].z, q[2].w};
+  double h = P[kMom - 1];
+#pragma unroll
+  for (int k = kMom - 2; k >= 0; --k) h = fma(h, na * kInvK[k], P[k]);  // P_k + (-a / (k + 1)) h
+  constexpr double kLog2e = 1.44269504088896340736;
+  return float(double(__builtin_amdgcn_exp2f(float(na * kLog2e))) * h);
+}
+static_assert(kMomR == 12 && kMom == 12, "record layout: P_0..P_11 in float4s 0..2, R in float4 3");
+
+// two workgroups per CU: 8 waves per SIMD, which needs <= 64 VGPRs and <= 80
+// SGPRs (MI355X_MICROARCH.md residency rules: 90 SGPRs admitted one)
+__global__ __launch_bounds__(64 * kKerWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_bkernel(Params p, int tb, int split, int scratch) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int waves = blockDim.x >> 6;
+  constexpr int NT = 64 * kKerWaves, Q = kFeatStride / 4;
   const int cand = blockIdx.x / split, part = blockIdx.x - cand * split;
-  const int b = p.b0 + cand, M = p.M, n = p.n, Md = dist_stride(M);
+  const int b = p.b0 + cand, M = p.M, n = p.n;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const KerLds C = ker_lds(M, n, waves);
+  const KerLds C = ker_lds(M, n, size_t(scratch));
   short* sl = reinterpret_cast<short*>(smem + C.sel);
   float* csg = reinterpret_cast<float*>(smem + C.csg);
-  uint32_t* pairs = reinterpret_cast<uint32_t*>(smem + C.pairs);
+  double* csd = reinterpret_cast<double*>(smem + C.csd);
+  unsigned short* tri = reinterpret_cast<unsigned short*>(smem + C.tri);
+  unsigned short* urank = reinterpret_cast<unsigned short*>(smem + C.urank);
+  unsigned short* urow = reinterpret_cast<unsigned short*>(smem + C.urow);
+  int* misc = reinterpret_cast<int*>(smem + C.misc);
+  unsigned char* uflag = reinterpret_cast<unsigned char*>(smem + C.scratch);  // setup only
+  const int ntri = tri_stride(n), nent = n * (n - 1) / 2;
+  const int s_lo = first_sample(tb);
+  const int i_lo = s_lo * n, i_hi = kBetaSamples * n;
+  MPCMMD_STAMP(p, 16);
+  MPCMMD_STAMPW(p, 0);
+  const int32_t* gsel = p.bsel + size_t(b) * kBetaSamples * n;
+  for (int i = i_lo + tid; i < i_hi; i += NT) sl[i] = short(gsel[i]);
+  for (int s = s_lo + tid; s < kBetaSamples; s += NT) {
+    const float sg = p.bsig[size_t(b) * kBetaSamples + s];
+    csg[s] = kNegLog2e / sg;
+    csd[s] = 1.0 / double(sg);
+  }
+  for (int k = 1 + w; k < n; k += kKerWaves)  // entry k (k - 1) / 2 + kk of the strict lower triangle
+    for (int kk = lane; kk < k; kk += 64) tri[k * (k - 1) / 2 + kk] = (unsigned short)(k | kk << 8);
+  for (int r = tid; r < M; r += NT) uflag[r] = 0;
+  if (tid < 3) misc[tid] = 0;
+  __syncthreads();
+  for (int i = i_lo + tid; i < i_hi; i += NT) uflag[sl[i]] = 1;
+  __syncthreads();
+  {  // union ranks: exclusive scan of the flags (thread runs, wave scans, wave totals)
+    const int per = (M + NT - 1) / NT, a = tid * per, e = min(M, a + per);
+    int sq = 0;
+    for (int r = a; r < e; ++r) sq += uflag[r];
+    int y = sq;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int yo = __shfl_up(y, o, 64);
+      if (lane >= o) y += yo;
+    }
+    if (lane == 63) misc[16 + w] = y;
+    __syncthreads();
+    int base = 0;
+    for (int v = 0; v < w; ++v) base += misc[16 + v];
+    y += base - sq;
+    if (tid == NT - 1) misc[0] = y + sq;
+    for (int r = a; r < e; ++r) {
+      if (uflag[r]) {
+        urank[r] = (unsigned short)y;
+        urow[y] = (unsigned short)r;
+        ++y;
+      }
+    }
+  }
+  __syncthreads();  // the flags are dead: the scratch now holds the union's records
+  MPCMMD_STAMPW(p, 1);
+  const int Uu = misc[0];
+  {
+    // the union's records: staged in LDS when they fit, else read in place
+    const float4* mom = reinterpret_cast<const float4*>(p.bmom + size_t(b) * M * kMomStride);
+    const bool staged = size_t(Uu) * kMomStride * 4 <= size_t(scratch);  // block-uniform
+    float4* lrec = reinterpret_cast<float4*>(smem + C.scratch);
+    if (staged)
+      for (int i = tid; i < Uu * 4; i += NT) lrec[i] = mom[size_t(urow[i >> 2]) * 4 + (i & 3)];
+    for (int i = i_lo + tid; i < i_hi; i += NT) sl[i] = short(urank[sl[i]]);  // rows -> union ranks
+    __syncthreads();
+    const float4* rec = staged ? lrec : mom;
+    // series pairs of this part's samples; the others flagged for k_bdirect
+    float* rowsum = p.brow + size_t(b) * kBetaSamples * n;
+    unsigned char* dflag = p.bdflag + size_t(b) * kBetaSamples * n;
+    int nd = 0;
+    const int ns = (kBetaSamples - s_lo - part + split - 1) / split;
+    for (int j = tid; j < ns * n; j += NT) {
+      const int sj = j / n, s = s_lo + part + split * sj, i = s * n + (j - sj * n);
+      const float4* q = rec + 4 * (staged ? int(sl[i]) : int(urow[sl[i]]));
+      const double na = -double(q[3].x) * csd[s];  // -a, a = R / sigma
+      const bool series = -na <= kSeriesAMax;     // NaN sigma: direct (NaN sum, as the reference)
+      if (series) {
+        const float4 qq[3] = {q[0], q[1], q[2]};
+        rowsum[i] = series_sum(qq, na);
+      }
+      dflag[i] = series ? 0 : 1;
+      nd += series ? 0 : 1;
+    }
+    nd = wave_total(nd);
+    if (lane == 0) atomicAdd(&misc[2], nd);
+    __syncthreads();  // the records are dead
+    if (tid == 0) {
+      p.bdcount[size_t(b) * kMaxSplit + part] = misc[2];
+      atomicAdd(&p.stats[2], static_cast<unsigned long long>(ns * n - misc[2]));
+      if (part == 0) atomicAdd(&p.stats[3], static_cast<unsigned long long>((kBetaSamples - s_lo) * nent));
+    }
+  }
+  MPCMMD_STAMP(p, 17);
+  MPCMMD_STAMPW(p, 2);
+  const float4* fg = reinterpret_cast<const float4*>(p.featr + size_t(b) * M * kFeatStride);
+  float* kbase = p.bkred + size_t(b) * kBetaSamples * ntri;
+  if (ker_tab_bytes(Uu) <= size_t(scratch)) {  // block-uniform
+    float* T = reinterpret_cast<float*>(smem + C.scratch);
+    float4* Fu = reinterpret_cast<float4*>(smem + C.scratch + ((size_t(Uu) * (Uu - 1) / 2 * 4 + 15) & ~size_t(15)));
+    for (int i = tid; i < Uu * Q; i += NT) {
+      const int u = i / Q;
+      Fu[i] = fg[size_t(urow[u]) * Q + (i - u * Q)];
+    }
+    __syncthreads();
+    // work items: (block of 64 rows a, chunk of 16 rows b below the block's last row)
+    const int nab = (Uu + 63) >> 6;
+    auto chunks = [&](int ab) { return (min(64 * ab + 63, Uu - 1) + 15) >> 4; };
+    int items = 0;
+    for (int ab = 0; ab < nab; ++ab) items += chunks(ab);
+    for (int it = w; it < items; it += kKerWaves) {
+      int ab = 0, c = it;
+      while (c >= chunks(ab)) c -= chunks(ab++);
+      const int a = 64 * ab + lane;
+      float fa[kF];
+      {
+        const float4* src = Fu + min(a, Uu - 1) * Q;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          const float4 v = src[q];
+          fa[4 * q] = v.x;
+          fa[4 * q + 1] = v.y;
+          if (q < Q - 1) {
+            fa[4 * q + 2] = v.z;
+            fa[4 * q + 3] = v.w;
+          }
+        }
+      }
+      const int b_end = min(16 * c + 16, min(64 * ab + 63, Uu - 1));
+      float* Ta = T + a * (a - 1) / 2;
+#pragma unroll 2
+      for (int bb = 16 * c; bb < b_end; ++bb) {
+        const float4* fb = Fu + bb * Q;  // wave-uniform: LDS broadcast
+        float dd = 0.0f;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {  // differences as packed pairs, the sum in feature order
+          const float4 y = fb[q];
+          const f2 d0 = f2{fa[4 * q], fa[4 * q + 1]} - f2{y.x, y.y};
+          dd = q == 0 ? fabsf(d0.x) : dd + fabsf(d0.x);
+          dd = dd + fabsf(d0.y);
+          if (q < Q - 1) {
+            const f2 d1 = f2{fa[4 * q + 2], fa[4 * q + 3]} - f2{y.z, y.w};
+            dd = dd + fabsf(d1.x);
+            dd = dd + fabsf(d1.y);
+          }
+        }
+        if (bb < a && a < Uu) Ta[bb] = dd;
+      }
+    }
+    __syncthreads();
+    MPCMMD_STAMPW(p, 3);
+    // a wave per sample of this part, all its lookups in flight together
+    // (entries lane + 64 j, j < kJ covers n <= 23; larger n loop)
+    constexpr int kJ = 4;
+    for (int s = s_lo + part + split * w; s < kBetaSamples; s += split * kKerWaves) {
+      const short* su = sl + s * n;
+      const float cs = csg[s];
+      float* kr = kbase + size_t(s) * ntri;
+      for (int e0 = 0; e0 < nent; e0 += 64 * kJ) {
+        int t[kJ];
+#pragma unroll
+        for (int j = 0; j < kJ; ++j) t[j] = tri[min(e0 + lane + 64 * j, nent - 1)];
+        int u0[kJ], u1[kJ];
+#pragma unroll
+        for (int j = 0; j < kJ; ++j) {
+          u0[j] = su[t[j] & 0xFF];
+          u1[j] = su[t[j] >> 8];
+        }
+        float dv[kJ];
+#pragma unroll
+        for (int j = 0; j < kJ; ++j) {
+          const int hi = max(u0[j], u1[j]), lo = min(u0[j], u1[j]);
+          dv[j] = T[hi * (hi - 1) / 2 + lo];
+        }
+#pragma unroll
+        for (int j = 0; j < kJ; ++j)
+          if (e0 + lane + 64 * j < nent) kr[e0 + lane + 64 * j] = __builtin_amdgcn_exp2f(dv[j] * cs);
+      }
+    }
+  } else {
+    // per-sample: the union records are dead, sl holds union ranks (urow maps back)
+    float4* Fw = reinterpret_cast<float4*>(smem + C.scratch) + size_t(w) * n * Q;
+    for (int s = s_lo + part + split * w; s < kBetaSamples; s += split * kKerWaves) {
+      for (int k = lane; k < n; k += 64) {
+        const float4* src = fg + size_t(urow[sl[s * n + k]]) * Q;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) Fw[k * Q + q] = src[q];
+      }
+      wave_sync();  // one wave's LDS operations run in order
+      const float cs = csg[s];
+      float* kr = kbase + size_t(s) * ntri;
+      for (int e = lane; e < nent; e += 64) {
+        const int kk2 = tri[e];
+        const float4* A = Fw + (kk2 & 0xFF) * Q;
+        const float4* Bv = Fw + (kk2 >> 8) * Q;
+        float dd = 0.0f;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          const float4 x = A[q], y = Bv[q];
+          dd = q == 0 ? fabsf(x.x - y.x) : dd + fabsf(x.x - y.x);
+          dd = dd + fabsf(x.y - y.y);
+          if (q < Q - 1) {  // features 22, 23 are padding
+            dd = dd + fabsf(x.z - y.z);
+            dd = dd + fabsf(x.w - y.w);
+          }
+        }
+        kr[e] = __builtin_amdgcn_exp2f(dd * cs);
+      }
+      wave_sync();  // the reads are done before the next sample's rows overwrite them
+    }
+  }
+  MPCMMD_STAMP(p, 18);
+  MPCMMD_STAMPW(p, 4);
+}
+
+template <int NV4>
+__global__ __launch_bounds__(64 * kDirWaves) void k_bdirect(Params p, int tb, int kparts, int split, int lpt) {
+  constexpr bool kPrefetch = NV4 <= 4;
+  constexpr int NT = 64 * kDirWaves;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int cand = blockIdx.x / split, part = blockIdx.x - cand * split;
+  const int b = p.b0 + cand, M = p.M, n = p.n, Md = dist_stride(M);
+  int total = 0;  // flagged pairs of the candidate (k_bkernel's parts)
+  for (int k = 0; k < kparts; ++k) total += p.bdcount[size_t(b) * kMaxSplit + k];
+  if (total == 0) return;  // block-uniform
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const DirLds C = dir_lds(M, n);
+  short* sl = reinterpret_cast<short*>(smem + C.sel);
+  float* csg = reinterpret_cast<float*>(smem + C.csg);
+  unsigned short* pairs = reinterpret_cast<unsigned short*>(smem + C.pairs);
   unsigned short* ulist = reinterpret_cast<unsigned short*>(smem + C.ulist);
   unsigned short* ustart = reinterpret_cast<unsigned short*>(smem + C.ustart);
   unsigned short* order = reinterpret_cast<unsigned short*>(smem + C.order);
   int* bins = reinterpret_cast<int*>(smem + C.bins);
-  int* misc = reinterpret_cast<int*>(smem + C.misc);  // [0] next row, [1] distinct rows
-  int* cnt = reinterpret_cast<int*>(smem + C.rowbuf);  // setup only
+  int* misc = reinterpret_cast<int*>(smem + C.misc);
+  int* cnt = reinterpret_cast<int*>(smem + C.scratch);  // setup only
   int* fill = cnt + M;
   unsigned short* start = reinterpret_cast<unsigned short*>(fill + M);
   float* rowsum = p.brow + size_t(b) * kBetaSamples * n;
-  const int ntri = tri_stride(n);
+  const unsigned char* dflag = p.bdflag + size_t(b) * kBetaSamples * n;
   const int s_lo = first_sample(tb);
   const int i_lo = s_lo * n, i_hi = kBetaSamples * n;
-  MPCMMD_STAMP(p, 16);
   const int32_t* gsel = p.bsel + size_t(b) * kBetaSamples * n;
-  for (int i = i_lo + tid; i < i_hi; i += blockDim.x) sl[i] = short(gsel[i]);
-  for (int s = s_lo + tid; s < kBetaSamples; s += blockDim.x)
-    csg[s] = kNegLog2e / p.bsig[size_t(b) * kBetaSamples + s];
-  for (int r = tid; r < M; r += blockDim.x) {
+  // direct pairs keep their row; the others get row -1
+  for (int i = i_lo + tid; i < i_hi; i += NT) sl[i] = dflag[i] ? short(gsel[i]) : short(-1);
+  for (int s = s_lo + tid; s < kBetaSamples; s += NT) csg[s] = kNegLog2e / p.bsig[size_t(b) * kBetaSamples + s];
+  for (int r = tid; r < M; r += NT) {
     cnt[r] = 0;
     fill[r] = 0;
   }
   if (tid == 0) misc[0] = 0;
-  for (int c = tid; c < kLptBins; c += blockDim.x) bins[c] = 0;
+  for (int c = tid; c < kLptBins; c += NT) bins[c] = 0;
   __syncthreads();
-  for (int i = i_lo + tid; i < i_hi; i += blockDim.x) atomicAdd(&cnt[sl[i]], 1);
+  for (int i = i_lo + tid; i < i_hi; i += NT)
+    if (sl[i] >= 0) atomicAdd(&cnt[sl[i]], 1);
   __syncthreads();
   {  // exclusive scans of cnt and (cnt > 0), packed as cnt | (cnt > 0) << 16
      // (totals <= 6400 pairs, <= 4096 rows): thread runs, wave scans, wave totals
-    const int nt = blockDim.x, per = (M + nt - 1) / nt, a = tid * per, e = min(M, a + per);
+    const int per = (M + NT - 1) / NT, a = tid * per, e = min(M, a + per);
     int sp = 0;
     for (int r = a; r < e; ++r) {
       const int c = cnt[r];
@@ -913,7 +1275,7 @@ __global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb,
     int base = 0;
     for (int v = 0; v < w; ++v) base += misc[16 + v];
     x += base - sp;  // exclusive prefix of this thread's run
-    if (tid == nt - 1) {
+    if (tid == NT - 1) {
       const int tot = x + sp;
       misc[1] = tot >> 16;
       ustart[tot >> 16] = (unsigned short)(tot & 0xFFFF);
@@ -932,22 +1294,19 @@ __global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb,
   const int U = misc[1];
   if (tid == 0 && part == 0) {
     atomicAdd(&p.stats[0], static_cast<unsigned long long>(U));
-    atomicAdd(&p.stats[1], static_cast<unsigned long long>(i_hi - i_lo));
+    atomicAdd(&p.stats[1], static_cast<unsigned long long>(total));
   }
-  for (int i = i_lo + tid; i < i_hi; i += blockDim.x) {
+  for (int i = i_lo + tid; i < i_hi; i += NT) {
     const int r = sl[i];
-    const int pos = start[r] + atomicAdd(&fill[r], 1);
-    const int s = i / n, k = i - s * n;  // i = s * n + k
-    // K_red offset of (s, k) | k << 18 | s << 24 (offset < 100 * 2016 < 2^18)
-    pairs[pos] = uint32_t(s * ntri + k * (k - 1) / 2) | uint32_t(k) << 18 | uint32_t(s) << 24;
+    if (r >= 0) pairs[start[r] + atomicAdd(&fill[r], 1)] = (unsigned short)i;
   }
-  // grab order: heaviest rows (most pairs) first, so no wave starts a long row
-  // while the others run dry (bucket sort by pair count; the order within a
-  // bucket is arbitrary -- every row's outputs are independent of it -- so
+  // grab order: heaviest rows (most pairs) first, so no wave starts a long
+  // row while the others run dry (bucket sort by pair count; the order within
+  // a bucket is arbitrary -- every row's outputs are independent of it -- so
   // only for a candidate in one workgroup: parts of a split candidate must
   // agree on the order)
   if (lpt && split == 1) {
-    for (int u = tid; u < U; u += blockDim.x) atomicAdd(&bins[kLptBins - 1 - min(ustart[u + 1] - ustart[u], kLptBins - 1)], 1);
+    for (int u = tid; u < U; u += NT) atomicAdd(&bins[kLptBins - 1 - min(ustart[u + 1] - ustart[u], kLptBins - 1)], 1);
     __syncthreads();
     if (tid < 64) {  // exclusive scan of the 128 bins, two per lane
       const int a = bins[2 * tid], c = bins[2 * tid + 1];
@@ -961,17 +1320,14 @@ __global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb,
       bins[2 * tid + 1] = x - c;
     }
     __syncthreads();
-    for (int u = tid; u < U; u += blockDim.x)
+    for (int u = tid; u < U; u += NT)
       order[atomicAdd(&bins[kLptBins - 1 - min(ustart[u + 1] - ustart[u], kLptBins - 1)], 1)] = (unsigned short)u;
   } else {
-    for (int u = tid; u < U; u += blockDim.x) order[u] = (unsigned short)u;
+    for (int u = tid; u < U; u += NT) order[u] = (unsigned short)u;
   }
-  __syncthreads();  // pairs built; the row buffers now overwrite the setup arrays
-  MPCMMD_STAMP(p, 17);
+  __syncthreads();
+  MPCMMD_STAMP(p, 19);
   const float4* Dg = reinterpret_cast<const float4*>(p.bdist + size_t(b) * M * Md);
-  float4* rb4 = reinterpret_cast<float4*>(smem + C.rowbuf) + size_t(w) * (Md >> 2);
-  const float* rb = reinterpret_cast<const float*>(rb4);
-  float* kbase = p.bkred + size_t(b) * kBetaSamples * ntri;
   // this part's rows order[part + split q], q from the workgroup's counter
   // (U: past the end)
   auto grab = [&]() {
@@ -985,23 +1341,14 @@ __global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb,
 #pragma unroll
     for (int t = 0; t < NV4; ++t) x[t] = src[64 * t];
   };
-  // one distinct row u held in x: its pairs 8 at a time, row sums and then
-  // the batch's K_red entries (8 lanes per pair, kk = lane & 7 + 8 i)
+  // one distinct row u held in x: its pairs 8 at a time
   auto do_row = [&](const float4 (&x)[NV4], int u) {
-    const float* rg = rb;  // the row the K_red gathers read: the wave's LDS copy, or the global row
-    if constexpr (NV4 <= kRowLdsMaxV4) {
-#pragma unroll
-      for (int t = 0; t < NV4; ++t) rb4[lane + 64 * t] = x[t];
-      wave_sync();  // the row copy is in LDS before the gathers (one wave's LDS operations run in order)
-    } else {
-      rg = reinterpret_cast<const float*>(Dg + size_t(ulist[u]) * (Md >> 2));
-    }
     const int pb = ustart[u], pc = ustart[u + 1] - pb;
     for (int c0 = 0; c0 < pc; c0 += 64) {  // (rows with more than 64 pairs: chunks)
       // lane l holds pair c0 + l and its scale; batches broadcast them by readlane
       const int cc = min(64, pc - c0);
-      const uint32_t pl = pairs[pb + c0 + min(lane, cc - 1)];
-      const float cl = csg[pl >> 24];
+      const int pl = pairs[pb + c0 + min(lane, cc - 1)];
+      const float cl = csg[pl / n];
       for (int j0 = 0; j0 < cc; j0 += 8) {
         float v[8];
 #pragma unroll
@@ -1026,17 +1373,10 @@ __global__ __launch_bounds__(64 * kKerWavesMax) void k_bkernel(Params p, int tb,
         const float sum = transpose_sum8(v);
         // lane group j = lane >> 3 takes pair j0 + j
         const int jg = j0 + (lane >> 3);
-        const bool live = jg < cc;
-        const uint32_t pkj = __shfl(pl, jg, 64);
-        const float cj = __shfl(cl, jg, 64);
-        const int s = pkj >> 24, k = live ? int(pkj >> 18) & 63 : 0;
-        if ((lane & 7) == 4 && live) rowsum[s * n + k] = sum;
-        const short* sls = sl + s * n;
-        float* kr = kbase + (pkj & 0x3FFFFu);
-        for (int kk = lane & 7; kk < k; kk += 8) kr[kk] = __builtin_amdgcn_exp2f(rg[sls[kk]] * cj);
+        const int pj = __shfl(pl, jg, 64);
+        if ((lane & 7) == 4 && jg < cc) rowsum[pj] = sum;
       }
     }
-    wave_sync();  // the gathers read the copy before the next row overwrites it
   };
   float4 d[NV4];
   int u = grab();
@@ -1816,7 +2156,7 @@ bool mmdopt_supported(int n, int H, int O, std::string* why) {
     if (why) *why = "mmd_opt needs num_reduced <= 64";
     return false;
   }
-  if (ker_lds(M, n, ker_waves(M, n)).total > kLdsBudget) {
+  if (dir_lds(M, n).total > kLdsBudget || ker_lds(M, n, ker_scratch(M, n, 1)).total > kLdsBudget) {
     if (why) *why = "mmd_opt: num_reduced^2 too large for the kernel-sum stage";
     return false;
   }
@@ -1837,6 +2177,28 @@ void launch_mother(const Params& p, int t, hipStream_t s) {
 void launch_bdist(const Params& p, hipStream_t s) {
   const int T = (p.M + kDistRows - 1) / kDistRows, groups = (p.Bt + kXcds - 1) / kXcds;
   hipLaunchKernelGGL(k_bdist, dim3(groups * T * kXcds), dim3(kDistThreads), 0, s, p);
+}
+
+template <int NV4>
+void launch_bmoment_v(const Params& p, hipStream_t s) {
+  const size_t rows = size_t(p.Bt) * p.M;
+  hipLaunchKernelGGL((k_bmoment<NV4>), dim3((rows + kMomRowsPerBlock - 1) / kMomRowsPerBlock),
+                     dim3(64 * kMomRowsPerBlock), 0, s, p);
+}
+
+void launch_bmoment(const Params& p, hipStream_t s) {
+  switch (dist_stride(p.M) >> 8) {
+#define MPCMMD_MOM_CASE(V) \
+  case V:                  \
+    return launch_bmoment_v<V>(p, s);
+    MPCMMD_MOM_CASE(1) MPCMMD_MOM_CASE(2) MPCMMD_MOM_CASE(3) MPCMMD_MOM_CASE(4)
+    MPCMMD_MOM_CASE(5) MPCMMD_MOM_CASE(6) MPCMMD_MOM_CASE(7) MPCMMD_MOM_CASE(8)
+    MPCMMD_MOM_CASE(9) MPCMMD_MOM_CASE(10) MPCMMD_MOM_CASE(11) MPCMMD_MOM_CASE(12)
+    MPCMMD_MOM_CASE(13) MPCMMD_MOM_CASE(14) MPCMMD_MOM_CASE(15)
+    default:
+      return launch_bmoment_v<16>(p, s);
+#undef MPCMMD_MOM_CASE
+  }
 }
 
 void launch_bsample(const Params& p, int tb, hipStream_t s) {
@@ -1920,27 +2282,37 @@ void launch_bqp(const Params& p, int tb, hipStream_t s) {
   }
 }
 
-template <int NV4>
-void launch_bkernel_v(const Params& p, int tb, int wv, int split, hipStream_t s) {
-  const KerLds k = ker_lds(p.M, p.n, wv);
-  hipLaunchKernelGGL((k_bkernel<NV4>), dim3(p.nb * split), dim3(64 * wv), k.total, s, p, tb, split, 1);
+// parts per candidate: enough workgroups to fill the chip
+int ker_split(int nb, int target) {
+  int split = 1;
+  while (split < kMaxSplit && nb * split < target) split <<= 1;
+  return split;
 }
 
 void launch_bkernel(const Params& p, int tb, hipStream_t s) {
-  const int wv = ker_waves(p.M, p.n);
-  // parts per candidate: enough workgroups to fill the chip
-  int split = 1;
-  while (split < 8 && p.nb * split < 512) split <<= 1;
+  const size_t sc = ker_scratch(p.M, p.n, tb);
+  hipLaunchKernelGGL(k_bkernel, dim3(p.nb * ker_split(p.nb, 512)), dim3(64 * kKerWaves), ker_lds(p.M, p.n, sc).total, s,
+                     p, tb, ker_split(p.nb, 512), int(sc));
+}
+
+template <int NV4>
+void launch_bdirect_v(const Params& p, int tb, int split, hipStream_t s) {
+  hipLaunchKernelGGL((k_bdirect<NV4>), dim3(p.nb * split), dim3(64 * kDirWaves), dir_lds(p.M, p.n).total, s, p, tb,
+                     ker_split(p.nb, 512), split, 1);
+}
+
+void launch_bdirect(const Params& p, int tb, hipStream_t s) {
+  const int split = ker_split(p.nb, 2048);
   switch (dist_stride(p.M) >> 8) {
 #define MPCMMD_KER_CASE(V) \
   case V:                  \
-    return launch_bkernel_v<V>(p, tb, wv, split, s);
+    return launch_bdirect_v<V>(p, tb, split, s);
     MPCMMD_KER_CASE(1) MPCMMD_KER_CASE(2) MPCMMD_KER_CASE(3) MPCMMD_KER_CASE(4)
     MPCMMD_KER_CASE(5) MPCMMD_KER_CASE(6) MPCMMD_KER_CASE(7) MPCMMD_KER_CASE(8)
     MPCMMD_KER_CASE(9) MPCMMD_KER_CASE(10) MPCMMD_KER_CASE(11) MPCMMD_KER_CASE(12)
     MPCMMD_KER_CASE(13) MPCMMD_KER_CASE(14) MPCMMD_KER_CASE(15)
     default:
-      return launch_bkernel_v<16>(p, tb, wv, split, s);
+      return launch_bdirect_v<16>(p, tb, split, s);
 #undef MPCMMD_KER_CASE
   }
 }

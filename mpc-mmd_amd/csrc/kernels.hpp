@@ -37,6 +37,13 @@ HDI_CONST int dist_stride(int M) { return (M + 255) & ~255; }
 // floats per sample of Params::bkred: the n (n - 1) / 2 strict lower triangle
 // rounded to whole 16-byte groups (the QP kernel stages rows as float4)
 HDI_CONST int tri_stride(int n) { return ((n * (n - 1) / 2) + 3) & ~3; }
+// floats per mother row of Params::featr (22 features, 2 zero pads: six float4)
+constexpr int kFeatStride = 24;
+// series record of a distance row (Params::bmom, k_bmoment): P_0..P_11, R, pad
+constexpr int kMom = 12;
+constexpr int kMomStride = 16;
+constexpr int kMomR = 12;
+constexpr int kMaxSplit = 8;  // workgroups per candidate of the row-sum kernels
 
 struct Params {
   // shapes / configuration.  A launch covers G configurations of B
@@ -97,6 +104,10 @@ struct Params {
                            //         runs of the beta-CEM part, compute_beta.py:133)
   // mmd_opt scratch (beta-CEM, compute_beta.py:93-157)
   float* feat;             // [B][22][M]   mother Bernstein coefficients (cx | cy)
+  float* featr;            // [B][M][kFeatStride] the same, row-major (K_red distances)
+  float* bmom;             // [B][M][kMomStride] series record of each distance row (k_bmoment)
+  unsigned char* bdflag;   // [B][100][n]  pairs k_bkernel left to k_bdirect (a > 1)
+  int32_t* bdcount;        // [B][kMaxSplit] their count per k_bkernel part
   float* bdist;            // [B][M][dist_stride(M)] L1 distances of the mother features
                            //              (kernel_computation.py:33-39), once per outer iteration
   float* ctrl_n;           // [B][2][n][H] noisy control rows (acc, steer)
@@ -115,8 +126,11 @@ struct Params {
   float* ygen;             // [B][kBzCols][ygs] new samples of the current beta-iteration (ygs = M+1 rounded to 32)
   // phase timestamps (s_memrealtime, 100 MHz) of workgroup 0, for profiling
   unsigned long long* dbg;  // [64]
+  unsigned long long* dbgw;  // [65536][8] per-workgroup phase stamps of one kernel (MPCMMD_STAMPW)
   // work counters for the roofline, summed over k_bkernel workgroups:
-  // [0] distinct distance rows staged, [1] (sample, reduced row) pairs summed
+  // [0] distinct distance rows summed directly, [1] (sample, reduced row) pairs
+  // summed directly (M exponentials each), [2] pairs summed by the series,
+  // [3] K_red entries
   unsigned long long* stats;  // [8]
   // outputs
   float* results;          // [G][T][kResultStride]
@@ -194,9 +208,11 @@ void launch_beta_planes(const Params& p, int t, hipStream_t s);
 // mmd_opt risk, one launch each (mpcmmd.hip chains them)
 void launch_mother(const Params& p, int t, hipStream_t s);
 void launch_bdist(const Params& p, hipStream_t s);
+void launch_bmoment(const Params& p, hipStream_t s);  // after launch_bdist: series records of the distance rows
 void launch_bsample(const Params& p, int tb, hipStream_t s);
 void launch_bselect(const Params& p, int tb, hipStream_t s);
-void launch_bkernel(const Params& p, int tb, hipStream_t s);
+void launch_bkernel(const Params& p, int tb, hipStream_t s);  // K_mixed row sums by the series, K_red
+void launch_bdirect(const Params& p, int tb, hipStream_t s);  // the other row sums, directly
 void launch_bqp(const Params& p, int tb, hipStream_t s);
 void launch_belite(const Params& p, int tb, hipStream_t s);
 void launch_bgen(const Params& p, int tb, hipStream_t s);  // + k_bsigma on the last beta-iteration

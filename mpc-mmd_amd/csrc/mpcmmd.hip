@@ -58,11 +58,13 @@ enum KernelId {
   kKGammaTab,
   kKBetaPlanes,
   kKBGen,
+  kKBMoment,
+  kKBDirect,
   kNumKernels
 };
 const char* kKernelNames[kNumKernels] = {"noise",   "front", "risk_baseline", "mother",   "bdist", "bsample",
                                          "bselect", "bkernel", "bqp",         "belite", "mmdfinal", "select",
-                                         "gamma_tab", "beta_planes", "bgen"};
+                                         "gamma_tab", "beta_planes", "bgen",    "bmoment",     "bdirect"};
 
 }  // namespace
 
@@ -242,6 +244,7 @@ void run_beta_iteration(mpcmmd_handle* h, const Params& p, int tb, hipStream_t s
   if (tb > 0) h->launch(kKBSample, [&] { launch_bsample(p, tb, st); });
   h->launch(kKBSelect, [&] { launch_bselect(p, tb, st); });
   h->launch(kKBKernel, [&] { launch_bkernel(p, tb, st); });
+  h->launch(kKBDirect, [&] { launch_bdirect(p, tb, st); });
   h->launch(kKBQp, [&] { launch_bqp(p, tb, st); });
   h->launch(kKBElite, [&] { launch_belite(p, tb, st); });
   h->launch(kKBGen, [&] { launch_bgen(p, tb, st); });
@@ -292,6 +295,7 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
         if (!h->mmd_ok) throw std::invalid_argument("mmd_opt unsupported for this configuration: " + h->mmd_why);
         h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
         h->launch(kKBDist, [&] { launch_bdist(p, h->stream); });
+        h->launch(kKBMoment, [&] { launch_bmoment(p, h->stream); });
         run_beta_cem(h);
         h->launch(kKMmdFinal, [&] { launch_mmdfinal(p, t, h->stream); });
       } else {
@@ -313,6 +317,7 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
         if (p.noise == MPCMMD_NOISE_BETA) h->launch(kKGammaTab, [&] { launch_gamma_tab(p, t, h->stream); });
         h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
         h->launch(kKBDist, [&] { launch_bdist(p, h->stream); });
+        h->launch(kKBMoment, [&] { launch_bmoment(p, h->stream); });
       }
       if (stage == 5) {  // samples + their top-n rows
         if (t > 0) h->launch(kKBSample, [&] { launch_bsample(p, t, h->stream); });
@@ -320,6 +325,7 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
       }
       if (stage == 6) {  // kernel sums + QP
         h->launch(kKBKernel, [&] { launch_bkernel(p, t, h->stream); });
+        h->launch(kKBDirect, [&] { launch_bdirect(p, t, h->stream); });
         h->launch(kKBQp, [&] { launch_bqp(p, t, h->stream); });
       }
       if (stage == 7) {
@@ -473,6 +479,10 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
       p.beta_z = (const double*)h->alloc("beta_z", size_t(kBetaIters) * pos_pad(h->M) * kBzCols * 8);
       const size_t M = h->M, M1 = M + 1, n = h->n;
       p.feat = (float*)h->alloc("feat", BT * 22 * M * 4);
+      p.featr = (float*)h->alloc("featr", BT * M * kFeatStride * 4);
+      p.bmom = (float*)h->alloc("bmom", BT * M * kMomStride * 4);
+      p.bdflag = (unsigned char*)h->alloc("bdflag", BT * kBetaSamples * n);
+      p.bdcount = (int32_t*)h->alloc("bdcount", BT * kMaxSplit * 4);
       p.bdist = (float*)h->alloc("bdist", BT * M * dist_stride(int(M)) * 4);
       p.ctrl_n = (float*)h->alloc("ctrl_n", BT * 2 * n * H * 4);
       p.bsel = (int32_t*)h->alloc("bsel", BT * kBetaSamples * n * 4);
@@ -509,6 +519,7 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     p.res_beta = (float*)h->alloc("res_beta", BT * kBetaIters * 4);
     p.btrace = (float*)h->alloc("btrace", BT * kBetaIters * 4);
     p.dbg = (unsigned long long*)h->alloc("dbg", 64 * 8);
+    p.dbgw = (unsigned long long*)h->alloc("dbgw", size_t(65536) * 8 * 8);
     p.stats = (unsigned long long*)h->alloc("stats", 8 * 8);
     p.results = (float*)h->alloc("results", size_t(GM) * T * kResultStride * 4);
     p.tr_proj = (int32_t*)h->alloc("tr_proj", size_t(GM) * T * B * 4);

@@ -339,8 +339,8 @@ class Handle:
         check(self._L.mpcmmd_profile(self._h, 1 if enable else 0))
 
     def kernel_times(self):
-        n = 16
+        n = 64
         la = (C.c_int32 * n)()
         ms = (C.c_double * n)()
-        k = check(self._L.mpcmmd_kernel_times(self._h, la, ms, n))
+        k = min(n, check(self._L.mpcmmd_kernel_times(self._h, la, ms, n)))
         return {self._L.mpcmmd_kernel_name(i).decode(): (la[i], ms[i]) for i in range(k)}

@@ -2,8 +2,8 @@
 """Phase stamps (s_memrealtime, 100 MHz) of workgroup 0 of the last launch of
 each beta-CEM kernel, after a few steps of a bench workload (GPU box):
     python tools/stamps.py [workload]
-Slots: 0-1 k_bsample, 16 k_bkernel start, 17 setup done, 18-19 (kernel
-specific), 20 end."""
+Slots: 0-1 k_bsample; k_bkernel 16 start, 19 series pairs done, 17 setup
+done, 18 K_red done, 20 end."""
 import os
 import sys
 
@@ -31,10 +31,8 @@ def main():
     h.close()
     us = lambda a, b: (d[b] - d[a]) / 100.0  # noqa: E731  (100 MHz ticks -> us)
     print(f"{name}: bsample {us(0, 1):.1f} us")
-    print(f"bkernel: setup {us(16, 17):.1f} us, rows {us(17, 20):.1f} us, total {us(16, 20):.1f} us")
-    for s in (18, 19):
-        if d[s] > d[16]:
-            print(f"  slot {s}: +{us(16, s):.1f} us")
+    print(f"bkernel: series {us(16, 19):.1f} us, scan/order {us(19, 17):.1f} us, K_red {us(17, 18):.1f} us, "
+          f"direct {us(18, 20):.1f} us, total {us(16, 20):.1f} us")
 
 
 if __name__ == "__main__":
