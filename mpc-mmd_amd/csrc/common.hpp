@@ -21,10 +21,11 @@ namespace mpcmmd {
 
 // per-workgroup phase timestamp into dbgw[blockIdx.x][slot] (profiling only;
 // the workgroups of one launch, slots 0..7)
-#define MPCMMD_STAMPW(p, slot)                                                  \
-  do {                                                                          \
-    if (threadIdx.x == 0 && (p).dbgw && blockIdx.x < 65536)                     \
-      (p).dbgw[size_t(blockIdx.x) * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+#define MPCMMD_STAMPW(p, slot)                                                      \
+  do {                                                                              \
+    const unsigned wg_ = blockIdx.x + gridDim.x * blockIdx.y;                       \
+    if (threadIdx.x == 0 && (p).dbgw && wg_ < 65536)                                \
+      (p).dbgw[size_t(wg_) * 8 + (slot)] = __builtin_amdgcn_s_memrealtime();        \
   } while (0)
 
 constexpr int kWave = 64;

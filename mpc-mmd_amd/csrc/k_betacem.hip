@@ -235,7 +235,12 @@ __global__ __launch_bounds__(kDistThreads) void k_bdist(Params p) {
 // directly).  One wave per row: the row as float4s in registers, the row max
 // by DPP, t and its powers in packed fp32 (the column pairs of a float4 as
 // one v_pk_* operand), one wave sum per moment.  Pad columns (+inf) count 0.
+// The first beta-iteration's pairs of the row (Params::rp0, the handle's
+// table) whose a > 1 are summed here directly, from the row already in
+// registers, instead of re-reading it in k_bdirect.
 constexpr int kMomRowsPerBlock = 4;
+constexpr double kSeriesAMaxRow = 1.0;                     // == kSeriesAMax (k_bkernel)
+constexpr float kNegLog2eRow = -1.44269504088896340736f;   // == kNegLog2e
 
 template <int NV4>
 __global__ __launch_bounds__(64 * kMomRowsPerBlock) void k_bmoment(Params p) {
@@ -288,6 +293,34 @@ __global__ __launch_bounds__(64 * kMomRowsPerBlock) void k_bmoment(Params p) {
   if (lane == 0) rec = float(M);
   if (lane == kMomR) rec = R;
   if (lane < kMomStride) p.bmom[(size_t(b) * M + r) * kMomStride + lane] = rec;
+  // first-iteration pairs of this row that the series does not cover (the
+  // test is k_bkernel's, on the same R and sigma)
+  const int n = p.n;
+  float* rowsum = p.brow + size_t(b) * kBetaSamples * n;
+  const int q0 = p.rp0[r], q1 = p.rp0[r + 1];
+  for (int c0 = q0; c0 < q1; c0 += 64) {  // the pairs' indices and sigmas loaded together, one per lane
+    const int il = p.rpair0[min(c0 + lane, q1 - 1)];
+    const float sl = p.sig0[il / n];
+    const bool dl = !(double(R) * (1.0 / double(sl)) <= kSeriesAMaxRow) && c0 + lane < q1;
+    unsigned long long todo = __ballot(dl);
+    while (todo) {  // wave-uniform
+      const int j = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const int i = __builtin_amdgcn_readlane(il, j);
+      const float sg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sl), j));
+      const float cs = kNegLog2eRow / sg;
+      const f2 c2 = {cs, cs};
+      f2 acc2 = {0.0f, 0.0f};
+#pragma unroll
+      for (int t = 0; t < NV4; ++t) {  // pad columns: +inf * cs = -inf -> 0
+        const f2 t0 = f2{x[t].x, x[t].y} * c2, t1 = f2{x[t].z, x[t].w} * c2;
+        acc2 += f2{__builtin_amdgcn_exp2f(t0.x), __builtin_amdgcn_exp2f(t0.y)};
+        acc2 += f2{__builtin_amdgcn_exp2f(t1.x), __builtin_amdgcn_exp2f(t1.y)};
+      }
+      const float sum = wave_total(acc2.x + acc2.y);
+      if (lane == 0) rowsum[i] = sum;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------
@@ -518,6 +551,20 @@ DEVI void select_walk(Row row, Out out, int first, int last, int stride, int M, 
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) key[q] = nxt[q];
+  }
+}
+
+// The first beta-iteration's selection from the handle's table (Params::sel0,
+// sig0: k_bselect's output for the shared initial samples, computed once per
+// table) into every candidate's bsel / bsig.
+__global__ __launch_bounds__(256) void k_bsel0(Params p) {
+  const int n = p.n, per = kBetaSamples * n + kBetaSamples;
+  for (size_t x = size_t(blockIdx.x) * 256 + threadIdx.x; x < size_t(p.nb) * per; x += size_t(gridDim.x) * 256) {
+    const int c = int(x / per), e = int(x - size_t(c) * per), b = p.b0 + c;
+    if (e < kBetaSamples * n)
+      p.bsel[size_t(b) * kBetaSamples * n + e] = p.sel0[e];
+    else
+      p.bsig[size_t(b) * kBetaSamples + e - kBetaSamples * n] = p.sig0[e - kBetaSamples * n];
   }
 }
 
@@ -872,7 +919,7 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
 constexpr int kKerWaves = 16;
 constexpr int kDirWaves = 4;
 constexpr int kLptBins = 128;        // pair counts per distinct row (<= 100 samples)
-constexpr double kSeriesAMax = 1.0;  // k_bmoment's error bound holds for a <= 1
+constexpr double kSeriesAMax = kSeriesAMaxRow;  // k_bmoment's error bound holds for a <= 1
 constexpr size_t kLdsBudget = 160 * 1024 - 1024;
 
 struct LdsTake {  // consecutive 16-byte aligned LDS pieces
@@ -945,7 +992,7 @@ HDI DirLds dir_lds(int M, int n) {
   return L;
 }
 
-constexpr float kNegLog2e = -1.44269504088896340736f;
+constexpr float kNegLog2e = kNegLog2eRow;
 
 DEVI float dpp_f_ror8(float v) { return __int_as_float(dpp_i<0x128>(__float_as_int(v))); }
 
@@ -1080,8 +1127,9 @@ __global__ __launch_bounds__(64 * kKerWaves) __attribute__((amdgpu_waves_per_eu(
         const float4 qq[3] = {q[0], q[1], q[2]};
         rowsum[i] = series_sum(qq, na);
       }
-      dflag[i] = series ? 0 : 1;
-      nd += series ? 0 : 1;
+      const bool direct = !series && tb > 0;  // first iteration: k_bmoment summed them
+      dflag[i] = direct ? 1 : 0;
+      nd += direct ? 1 : 0;
     }
     nd = wave_total(nd);
     if (lane == 0) atomicAdd(&misc[2], nd);
@@ -2215,6 +2263,11 @@ void launch_bsample(const Params& p, int tb, hipStream_t s) {
 // waves per candidate: ~16 single-wave workgroups per SIMD over the launch,
 // at most 16 per candidate (B = 1024: 8 -> 16 measured -8.5%; the 512-candidate
 // groups of the two-stream split: 25 -> 16 +1%)
+void launch_bsel0(const Params& p, hipStream_t s) {
+  const size_t total = size_t(p.nb) * (kBetaSamples * p.n + kBetaSamples);
+  hipLaunchKernelGGL(k_bsel0, dim3(unsigned(std::min<size_t>((total + 255) / 256, 4096))), dim3(256), 0, s, p);
+}
+
 int sel_waves(int nb) { return std::max(4, std::min(16, 16384 / std::max(1, nb))); }
 
 template <int NQ>

@@ -107,6 +107,13 @@ struct Params {
   float* featr;            // [B][M][kFeatStride] the same, row-major (K_red distances)
   float* bmom;             // [B][M][kMomStride] series record of each distance row (k_bmoment)
   unsigned char* bdflag;   // [B][100][n]  pairs k_bkernel left to k_bdirect (a > 1)
+  // the first beta-iteration's selection: its samples are the fixed-key
+  // normals beta_z0 (shared by every candidate, Q3), so the top-n rows and
+  // sigma are one table per handle, and the pairs are indexed by mother row
+  const int32_t* sel0;     // [100][n]     top-n rows of sample s (argsort order)
+  const float* sig0;       // [100]        its sigma
+  const int32_t* rp0;      // [M+1]        pairs of mother row r: rpair0[rp0[r] .. rp0[r+1])
+  const int32_t* rpair0;   // [100 n]      pair index i = s n + k, grouped by row
   int32_t* bdcount;        // [B][kMaxSplit] their count per k_bkernel part
   float* bdist;            // [B][M][dist_stride(M)] L1 distances of the mother features
                            //              (kernel_computation.py:33-39), once per outer iteration
@@ -211,6 +218,7 @@ void launch_bdist(const Params& p, hipStream_t s);
 void launch_bmoment(const Params& p, hipStream_t s);  // after launch_bdist: series records of the distance rows
 void launch_bsample(const Params& p, int tb, hipStream_t s);
 void launch_bselect(const Params& p, int tb, hipStream_t s);
+void launch_bsel0(const Params& p, hipStream_t s);  // first beta-iteration: the handle's table into bsel / bsig
 void launch_bkernel(const Params& p, int tb, hipStream_t s);  // K_mixed row sums by the series, K_red
 void launch_bdirect(const Params& p, int tb, hipStream_t s);  // the other row sums, directly
 void launch_bqp(const Params& p, int tb, hipStream_t s);

@@ -85,6 +85,7 @@ struct mpcmmd_handle {
   int last_t = -1;
   bool ext_roll = false, ext_res = false;
   bool beta_tables_internal = false;  // device beta tables hold the internal streams
+  bool sel0_valid = false;            // sel0 / sig0 / rp0 / rpair0 match the device beta_z0
   bool mmd_ok = false;                // mmd_opt buffers allocated (mmdopt_supported)
   std::string mmd_why;
   // pinned staging for the per-solve uploads of mpcmmd_begin: the copies are
@@ -237,14 +238,47 @@ void gen_beta_tables(mpcmmd_handle* h) {
   }
   HIPC(hipStreamSynchronize(h->stream));
   h->beta_tables_internal = true;
+  h->sel0_valid = false;
+}
+
+// The first beta-iteration's selection (samples sqrt(20) beta_z0, shared by
+// every candidate): k_bselect on one candidate, read back, and its pairs
+// indexed by mother row for k_bmoment.  Once per beta_z0 table.
+void ensure_sel0(mpcmmd_handle* h) {
+  if (h->sel0_valid) return;
+  const int n = h->n, M = h->M, np = kBetaSamples * n;
+  Params q = h->p;
+  q.b0 = 0;
+  q.nb = 1;
+  launch_bselect(q, 0, h->stream);
+  HIPC(hipGetLastError());
+  std::vector<int32_t> sel(np);
+  std::vector<float> sig(kBetaSamples);
+  HIPC(hipMemcpyAsync(sel.data(), h->p.bsel, np * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPC(hipMemcpyAsync(sig.data(), h->p.bsig, kBetaSamples * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPC(hipStreamSynchronize(h->stream));
+  std::vector<int32_t> rp(M + 1, 0), pairs(np);
+  for (int i = 0; i < np; ++i) {
+    if (sel[i] < 0 || sel[i] >= M) throw std::runtime_error("first beta-iteration selection out of range");
+    ++rp[sel[i] + 1];
+  }
+  for (int r = 0; r < M; ++r) rp[r + 1] += rp[r];
+  std::vector<int32_t> fill(rp.begin(), rp.end() - 1);
+  for (int i = 0; i < np; ++i) pairs[fill[sel[i]]++] = i;
+  upload(h, "sel0", sel.data(), np * 4);
+  upload(h, "sig0", sig.data(), kBetaSamples * 4);
+  upload(h, "rp0", rp.data(), (M + 1) * 4);
+  upload(h, "rpair0", pairs.data(), np * 4);
+  HIPC(hipStreamSynchronize(h->stream));  // host temporaries
+  h->sel0_valid = true;
 }
 
 // one beta-CEM iteration (compute_beta.py:112-147) of candidates [p.b0, p.b0 + p.nb)
 void run_beta_iteration(mpcmmd_handle* h, const Params& p, int tb, hipStream_t st) {
   if (tb > 0) h->launch(kKBSample, [&] { launch_bsample(p, tb, st); });
-  h->launch(kKBSelect, [&] { launch_bselect(p, tb, st); });
+  h->launch(kKBSelect, [&] { tb == 0 ? launch_bsel0(p, st) : launch_bselect(p, tb, st); });
   h->launch(kKBKernel, [&] { launch_bkernel(p, tb, st); });
-  h->launch(kKBDirect, [&] { launch_bdirect(p, tb, st); });
+  if (tb > 0) h->launch(kKBDirect, [&] { launch_bdirect(p, tb, st); });  // first iteration: in k_bmoment
   h->launch(kKBQp, [&] { launch_bqp(p, tb, st); });
   h->launch(kKBElite, [&] { launch_belite(p, tb, st); });
   h->launch(kKBGen, [&] { launch_bgen(p, tb, st); });
@@ -293,6 +327,7 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
       if (p.noise == MPCMMD_NOISE_BETA) h->launch(kKGammaTab, [&] { launch_gamma_tab(p, t, h->stream); });
       if (p.cost == MPCMMD_COST_MMD_OPT) {
         if (!h->mmd_ok) throw std::invalid_argument("mmd_opt unsupported for this configuration: " + h->mmd_why);
+        ensure_sel0(h);
         h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
         h->launch(kKBDist, [&] { launch_bdist(p, h->stream); });
         h->launch(kKBMoment, [&] { launch_bmoment(p, h->stream); });
@@ -315,17 +350,19 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
       if (stage >= 5 && stage <= 7 && t >= kBetaIters) throw std::invalid_argument("beta-CEM iteration out of range");
       if (stage == 4) {  // mother rollouts, features and their distance matrix
         if (p.noise == MPCMMD_NOISE_BETA) h->launch(kKGammaTab, [&] { launch_gamma_tab(p, t, h->stream); });
+        ensure_sel0(h);
         h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
         h->launch(kKBDist, [&] { launch_bdist(p, h->stream); });
         h->launch(kKBMoment, [&] { launch_bmoment(p, h->stream); });
       }
       if (stage == 5) {  // samples + their top-n rows
         if (t > 0) h->launch(kKBSample, [&] { launch_bsample(p, t, h->stream); });
-        h->launch(kKBSelect, [&] { launch_bselect(p, t, h->stream); });
+        if (t == 0) ensure_sel0(h);
+        h->launch(kKBSelect, [&] { t == 0 ? launch_bsel0(p, h->stream) : launch_bselect(p, t, h->stream); });
       }
       if (stage == 6) {  // kernel sums + QP
         h->launch(kKBKernel, [&] { launch_bkernel(p, t, h->stream); });
-        h->launch(kKBDirect, [&] { launch_bdirect(p, t, h->stream); });
+        if (t > 0) h->launch(kKBDirect, [&] { launch_bdirect(p, t, h->stream); });
         h->launch(kKBQp, [&] { launch_bqp(p, t, h->stream); });
       }
       if (stage == 7) {
@@ -483,6 +520,10 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
       p.bmom = (float*)h->alloc("bmom", BT * M * kMomStride * 4);
       p.bdflag = (unsigned char*)h->alloc("bdflag", BT * kBetaSamples * n);
       p.bdcount = (int32_t*)h->alloc("bdcount", BT * kMaxSplit * 4);
+      p.sel0 = (const int32_t*)h->alloc("sel0", size_t(kBetaSamples) * n * 4);
+      p.sig0 = (const float*)h->alloc("sig0", size_t(kBetaSamples) * 4);
+      p.rp0 = (const int32_t*)h->alloc("rp0", (M + 1) * 4);
+      p.rpair0 = (const int32_t*)h->alloc("rpair0", size_t(kBetaSamples) * n * 4);
       p.bdist = (float*)h->alloc("bdist", BT * M * dist_stride(int(M)) * 4);
       p.ctrl_n = (float*)h->alloc("ctrl_n", BT * 2 * n * H * 4);
       p.bsel = (int32_t*)h->alloc("bsel", BT * kBetaSamples * n * 4);
@@ -708,6 +749,7 @@ int begin_impl(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t
         for (int t = 0; t < kBetaIters; ++t)
           upload_beta_z(h, t, draws->beta_z + size_t(t) * (kBetaSamples - kBetaElite) * M1);
         h->beta_tables_internal = false;
+        h->sel0_valid = false;
       } else if (!h->beta_tables_internal) {
         gen_beta_tables(h);
       }
@@ -890,6 +932,7 @@ int mpcmmd_write(mpcmmd_handle* h, const char* name, const void* src, size_t byt
     HIPC(hipStreamSynchronize(h->stream));
     HIPC(hipMemcpy(it->second.first, src, bytes, hipMemcpyHostToDevice));
     if (std::string(name) == "beta_z0" || std::string(name) == "beta_z") h->beta_tables_internal = false;
+    if (std::string(name) == "beta_z0") h->sel0_valid = false;
     return MPCMMD_OK;
   });
 }
