@@ -90,7 +90,12 @@ def kernel_work(w, name, launches, stats):
                fp32 + n^2 cost FMAs in fp64 (each worth two fp32 issue
                slots), in fp32 lane-FMA equivalents against the fp32 rate
       bdist    M x M distances x 22 features x 2 (sub, abs-add) per candidate
-      beta_planes  B x S x H x 2 Beta draws x 37 fp64 lane-ops
+      bmoment  the distance matrix read once (M x dist_stride(M) x 4 B per
+               candidate) against HBM
+      beta_planes  B x S x H x 2 Beta draws x 27 VALU issue slots (attempt 0
+               of two gammas: 5 fp64 ops each; the combine: 6 fp64 ops and 11
+               fp32 slots, the four transcendentals at their double issue
+               cost) against one lane-slot per lane and cycle (39.3 T/s)
       risk_baseline  B x S rollouts x H steps x (bicycle 40 + 9 per obstacle (+ beta 320))"""
     B, H, O = w["num_batch"], w["num_prime"], w["num_obs"]
     n = w["num_reduced"]
@@ -108,8 +113,10 @@ def kernel_work(w, name, launches, stats):
         return "valu-fp32", "T lane-FMA/s", launches * B * per, VALU_PEAK_TOPS
     if name == "bdist":
         return "valu", "T lane-ops/s", launches * B * M * M * kF * 2, VALU_PEAK_TOPS
+    if name == "bmoment":
+        return "hbm", "GB/s", launches * B * M * ((M + 255) // 256 * 256) * 4, HBM_PEAK_GBS, 1e9
     if name == "beta_planes":
-        return "valu-fp64", "T lane-ops/s", launches * B * n * H * 2 * 37, VALU64_PEAK_TOPS
+        return "valu-issue", "T lane-slots/s", launches * B * n * H * 2 * 27, VALU64_PEAK_TOPS
     if name == "risk_baseline":
         beta = 2 * 160 if w["noise"] == "beta" else 0
         return "valu", "T lane-ops/s", launches * B * n * H * (40 + O * 9 + beta), VALU_PEAK_TOPS
