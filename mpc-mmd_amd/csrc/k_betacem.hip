@@ -1987,122 +1987,94 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
   }
 }
 
-// k_bgen: level 2 of the generators, one thread per (candidate, block of 16
-// positions).  The block prefix Phi_b (k_belite) is factored once and
-// inverted, A = Phi_b^-1; then, position by position through the block,
+// k_bgen: level 2 of the generators, one quad (4 lanes) per (candidate,
+// block of 16 positions).  The block prefix Phi_b (k_belite) is inverted
+// once, A = Phi_b^-1; then, position by position through the block,
 //   v_j = A u_j,  L_jj = sqrt(0.05 + u_j . v_j),  w_j = v_j / L_jj,
 //   A <- A - w_j w_j^T      (= Phi_{j+1}^-1: Sherman-Morrison, since
 //                            Phi_{j+1} = Phi_j + u_j u_j^T / 0.05)
-// -- at most 15 rank-1 steps from an exactly factored start, so the error
-// stays at the level of one fp64 Cholesky.  Each block is a short sequential
-// chain; the ~32 blocks per candidate run in parallel.
+// -- at most 15 rank-1 steps from an exactly inverted start, so the error
+// stays at the level of one fp64 inversion.  Lane q of the quad owns rows
+// q, q + 4, q + 8 of A (full rows, so A stays symmetric without a packed
+// layout); the inverse is an in-place Gauss-Jordan sweep (Phi_b is SPD: no
+// pivoting), its pivot rows and the w_j of each step quad broadcasts (DPP),
+// so the chain per position is one 11-term dot product deep instead of the
+// whole matrix-vector product, and the ~32 blocks x 4 lanes of a candidate
+// give ~2 waves per SIMD at B = 1024 (one lane per block gave < 1).
 HDI int sym11i(int a, int c) { return a <= c ? sym11(a, c) : sym11(c, a); }
 
-__global__ __launch_bounds__(64) void k_bgen(Params p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_bgen(Params p) {
   const int M = p.M, M1 = M + 1, nblk = (M1 + 15) / 16;
-  const int gid = blockIdx.x * 64 + threadIdx.x;
-  if (gid >= p.nb * nblk) return;
-  const int b = p.b0 + gid / nblk, blk = gid % nblk;
+  const int gq = (blockIdx.x * blockDim.x + threadIdx.x) >> 2, q = threadIdx.x & 3;
+  const bool live = gq < p.nb * nblk;  // quads stay whole: dead ones compute on a clamped block, store nothing
+  const int gqc = live ? gq : p.nb * nblk - 1;
+  const int b = p.b0 + gqc / nblk, blk = gqc % nblk;
   double* gen = p.gen + size_t(b) * pos_pad(M) * kGenStride;
   const double* Gb = p.phib + (size_t(b) * nblk + blk) * 66;
-  double A[66];
+  // own rows a = q + 4 i; row 11 (q = 3, i = 2) is padding: an identity row
+  // that no other row reads (column 11 does not exist)
+  double A[3][11];
 #pragma unroll
-  for (int e = 0; e < 66; ++e) A[e] = Gb[e];
-  // Cholesky Phi_b = R^T R (R upper, in A; rinv = 1 / diag)
-  double rinv[11];
+  for (int i = 0; i < 3; ++i) {
+    const int a = q + 4 * i;
 #pragma unroll
-  for (int a = 0; a < 11; ++a) {
-    double d = A[sym11(a, a)];
+    for (int c = 0; c < 11; ++c) A[i][c] = a < 11 ? Gb[sym11i(a, c)] : 0.0;
+  }
+  // in-place Gauss-Jordan inversion
 #pragma unroll
-    for (int k = 0; k < a; ++k) d = fma(-A[sym11(k, a)], A[sym11(k, a)], d);
-    d = sqrt(d);
-    A[sym11(a, a)] = d;
-    rinv[a] = 1.0 / d;
+  for (int k = 0; k < 11; ++k) {
+    const int ik = k >> 2, ok = k & 3;
+    const double ip = 1.0 / quad_bcast(A[ik][k], ok);  // the pivot, from its owner lane
+    double f[3];
 #pragma unroll
-    for (int c = a + 1; c < 11; ++c) {
-      double s = A[sym11(a, c)];
+    for (int i = 0; i < 3; ++i) f[i] = A[i][k];
+    // column by column: entry c of pivot row k (broadcast before its owner
+    // overwrites it), scaled, then every own row's update
 #pragma unroll
-      for (int k = 0; k < a; ++k) s = fma(-A[sym11(k, a)], A[sym11(k, c)], s);
-      A[sym11(a, c)] = s * rinv[a];
+    for (int c = 0; c < 11; ++c) {
+      const double rc = c == k ? ip : quad_bcast(A[ik][c], ok) * ip;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const bool pivot_row = q + 4 * i == k;
+        A[i][c] = pivot_row ? rc : (c == k ? -f[i] * ip : fma(-f[i], rc, A[i][c]));
+      }
     }
   }
-  // X = R^-1 (upper), column by column: X_cc = 1 / R_cc, X_ac = -(sum_{a<k<=c} R_ak X_kc) / R_aa
-  double X[66];
-#pragma unroll
-  for (int c = 0; c < 11; ++c) {
-    X[sym11(c, c)] = rinv[c];
-#pragma unroll
-    for (int a = c - 1; a >= 0; --a) {
-      double s = 0.0;
-#pragma unroll
-      for (int k = a + 1; k <= c; ++k) s = fma(A[sym11(a, k)], X[sym11(k, c)], s);
-      X[sym11(a, c)] = -s * rinv[a];
-    }
-  }
-  // A = Phi_b^-1 = X X^T (symmetric, packed upper)
-#pragma unroll
-  for (int a = 0; a < 11; ++a)
-#pragma unroll
-    for (int c = a; c < 11; ++c) {
-      double s = 0.0;
-#pragma unroll
-      for (int k = c; k < 11; ++k) s = fma(X[sym11(a, k)], X[sym11(c, k)], s);
-      A[sym11(a, c)] = s;
-    }
   const int j0 = blk * 16, j1 = min(M1, j0 + 16);
-  // u of the block's positions in groups of four, the next group's loads in
-  // flight while one group is processed (one memory latency per block, not
-  // one per position; positions past the block end re-read the last one)
-  auto load4 = [&](double (&uu)[4][11], int grp) {
+  for (int j = j0; j < j1; ++j) {
+    double u[11];  // the quad's four lanes load the same 88 bytes
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int jc = min(j0 + 4 * grp + jj, j1 - 1);
+    for (int c = 0; c < 11; ++c) u[c] = gen[size_t(j) * kGenStride + kGenU + c];
+    double v[3], part = 0.0;
 #pragma unroll
-      for (int a = 0; a < 11; ++a) uu[jj][a] = gen[size_t(jc) * kGenStride + kGenU + a];
+    for (int i = 0; i < 3; ++i) {
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c < 11; ++c) s = fma(A[i][c], u[c], s);
+      v[i] = s;
+      const int a = q + 4 * i;
+      part = fma(a < 11 ? u[min(a, 10)] : 0.0, s, part);
     }
-  };
-  auto step4 = [&](const double (&uu)[4][11], int grp) {
+    const double uv = quad_sum(part);
+    const double ljj = sqrt(kRidge + uv);
+    const double rl = 1.0 / ljj;
+    double w[3];
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int j = j0 + 4 * grp + jj;
-      if (j >= j1) break;
-      const double* u = uu[jj];
-      double v[11];
+    for (int i = 0; i < 3; ++i) w[i] = v[i] * rl;
+    double* g = gen + size_t(j) * kGenStride;
+    if (live) {
 #pragma unroll
-      for (int a = 0; a < 11; ++a) {
-        double s = 0.0;
-#pragma unroll
-        for (int c = 0; c < 11; ++c) s = fma(A[sym11i(a, c)], u[c], s);
-        v[a] = s;
-      }
-      double uv = 0.0;
-#pragma unroll
-      for (int a = 0; a < 11; ++a) uv = fma(u[a], v[a], uv);
-      const double ljj = sqrt(kRidge + uv);
-      const double rl = 1.0 / ljj;
-      double* g = gen + size_t(j) * kGenStride;
-      double w[11];
-#pragma unroll
-      for (int a = 0; a < 11; ++a) {
-        w[a] = v[a] * rl;
-        g[kGenW + a] = w[a];
-      }
-      g[kGenL] = ljj;
-#pragma unroll
-      for (int a = 0; a < 11; ++a)
-#pragma unroll
-        for (int c = a; c < 11; ++c) A[sym11(a, c)] = fma(-w[a], w[c], A[sym11(a, c)]);
+      for (int i = 0; i < 3; ++i)
+        if (q + 4 * i < 11) g[kGenW + q + 4 * i] = w[i];
+      if (q == 0) g[kGenL] = ljj;
     }
-  };
-  double ua[4][11], ub[4][11];
-  load4(ua, 0);
-  load4(ub, 1);
-  step4(ua, 0);
-  load4(ua, 2);
-  step4(ub, 1);
-  load4(ub, 3);
-  step4(ua, 2);
-  step4(ub, 3);
+#pragma unroll
+    for (int c = 0; c < 11; ++c) {
+      const double wc = quad_bcast(w[c >> 2], c & 3);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) A[i][c] = fma(-w[i], wc, A[i][c]);
+    }
+  }
 }
 
 // k_bsigma (last beta-iteration only): sigma_best when argmin is a new
@@ -2377,7 +2349,7 @@ void launch_belite(const Params& p, int tb, hipStream_t s) {
 
 void launch_bgen(const Params& p, int tb, hipStream_t s) {
   const int nblk = (p.M + 1 + 15) / 16;
-  hipLaunchKernelGGL(k_bgen, dim3((p.nb * nblk + 63) / 64), dim3(64), 0, s, p);
+  hipLaunchKernelGGL(k_bgen, dim3((p.nb * nblk * 4 + 255) / 256), dim3(256), 0, s, p);
   if (tb == kBetaIters - 1) hipLaunchKernelGGL(k_bsigma, dim3(p.nb), dim3(kThreads), 0, s, p, tb);
 }
 
