@@ -461,7 +461,7 @@ DEVI bool emit_window(const uint32_t* key, uint32_t T, int n, int32_t* out, unsi
     c += __popcll(m);
   }
   if (c > cap) return false;
-  if (lane < 2) cand[c + lane] = 0ull;  // pad the pair read past c (ranks nothing: real keys have bit 31 set)
+  if (lane < 8) cand[c + lane] = 0ull;  // pad the reads past c (rank nothing: real keys have bit 31 set)
   wave_sync();
   unsigned long long mine[R];
   int rank[R];
@@ -471,10 +471,14 @@ DEVI bool emit_window(const uint32_t* key, uint32_t T, int n, int32_t* out, unsi
     rank[r] = 0;
   }
   const ulonglong2* c2 = reinterpret_cast<const ulonglong2*>(cand);
-  for (int e = 0; e < c; e += 2) {
-    const ulonglong2 v = c2[e >> 1];  // wave-uniform address: LDS broadcast
+  for (int e = 0; e < c; e += 8) {  // four broadcast reads in flight, not one LDS latency per pair
+    ulonglong2 v[4];
 #pragma unroll
-    for (int r = 0; r < R; ++r) rank[r] += int(v.x > mine[r]) + int(v.y > mine[r]);
+    for (int u = 0; u < 4; ++u) v[u] = c2[(e >> 1) + u];  // wave-uniform address: LDS broadcast
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r) rank[r] += int(v[u].x > mine[r]) + int(v[u].y > mine[r]);
   }
 #pragma unroll
   for (int r = 0; r < R; ++r)
@@ -851,7 +855,7 @@ __global__ __launch_bounds__(64 * kChunkWavesMax) void k_bsample_chunks(Params p
 // has its own register allocation
 template <int NQ, int R, int G>
 __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
-  __shared__ __attribute__((aligned(16))) unsigned long long cand[64 * R + 4];
+  __shared__ __attribute__((aligned(16))) unsigned long long cand[64 * R + 8];
   __shared__ __attribute__((aligned(16))) uint32_t lm[64];
   __shared__ int scratch[128];
   const int b = p.b0 + blockIdx.x, g = blockIdx.y, W = gridDim.y, M = p.M, M1 = M + 1, n = p.n;
@@ -1816,19 +1820,28 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
   int* info = elite + 16;                                 // [0] imin, [1] any NaN
   float* cst = reinterpret_cast<float*>(info + 16);       // [100]
   float* sig_new = cst + kBetaSamples;                    // [11] sigma of the new elite rows
+  uint32_t* ckey = reinterpret_cast<uint32_t*>(sig_new + 12);  // [100] sort keys of the costs (16-byte aligned)
   const float* costs = p.bcost + size_t(b) * kBetaSamples;
-  if (tid < kBetaSamples) cst[tid] = costs[tid];
+  if (tid < kBetaSamples) {
+    const float c = costs[tid];
+    cst[tid] = c;
+    ckey[tid] = sort_key(c);
+  }
   if (tid == 0) {
     info[0] = -1;
     info[1] = 0;
   }
   __syncthreads();
   if (tid < kBetaSamples) {
-    const uint32_t ks = sort_key(cst[tid]);
+    // stable rank: 25 broadcast reads of four keys each, all in flight
+    const uint32_t ks = ckey[tid];
+    const uint4* k4 = reinterpret_cast<const uint4*>(ckey);
     int r = 0;
-    for (int k = 0; k < kBetaSamples; ++k) {
-      const uint32_t kk = sort_key(cst[k]);
-      r += (kk < ks) || (kk == ks && k < tid);
+#pragma unroll
+    for (int k = 0; k < kBetaSamples / 4; ++k) {
+      const uint4 v = k4[k];
+      r += int(v.x < ks || (v.x == ks && 4 * k < tid)) + int(v.y < ks || (v.y == ks && 4 * k + 1 < tid)) +
+           int(v.z < ks || (v.z == ks && 4 * k + 2 < tid)) + int(v.w < ks || (v.w == ks && 4 * k + 3 < tid));
     }
     if (r < kBetaElite) elite[r] = tid;
     if (cst[tid] != cst[tid]) {
@@ -1966,7 +1979,8 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
     c += a;
     double acc = a == c ? 1.0 : 0.0;
     double* ph = p.phib + size_t(b) * nblk * 66;
-    for (int blk = 0; blk < nblk; ++blk) {
+#pragma unroll 8
+    for (int blk = 0; blk < nblk; ++blk) {  // the LDS reads of several blocks in flight
       const double g = Gb[blk * 66 + tid];
       ph[blk * 66 + tid] = acc;
       acc = fma(g, kInvRidge, acc);
