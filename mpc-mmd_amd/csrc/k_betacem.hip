@@ -1520,26 +1520,26 @@ DEVI void bqp_quad(const Params& p, int tb, float* kl) {
   const int gqc = ok ? gq : 0;
   const int b = p.b0 + gqc / per, s = s_lo + gqc % per;
   const int ntri = tri_stride(n);
-  {  // wave w copies the rows of QPs w, w + W, ... as float4s, four rows in flight
+  {  // the workgroup's K_red rows as float4s, consecutive threads on consecutive
+     // float4s, every thread's loads issued before its first LDS store (one
+     // memory latency, not one per four rows)
     const int nq = blockDim.x >> 2, q0 = blockIdx.x * nq, total = p.nb * per, n4 = ntri >> 2;
-    const int lane = threadIdx.x & 63, W = blockDim.x >> 6;
     float4* kl4 = reinterpret_cast<float4*>(kl);
-    for (int c0 = 0; c0 < n4; c0 += 64) {
-      const int c = min(c0 + lane, n4 - 1);
-      for (int j0 = 0; j0 < nq; j0 += W * 4) {
-        float4 v[4];
+    constexpr int kU = 16;  // float4s per thread and round: 32 QPs x 58 float4s fit one round at n = 22
+    for (int i0 = 0; i0 < nq * n4; i0 += kU * int(blockDim.x)) {
+      float4 v[kU];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int j = j0 + (threadIdx.x >> 6) + W * u, g = min(q0 + min(j, nq - 1), total - 1);
-          const float4* src = reinterpret_cast<const float4*>(
-              p.bkred + (size_t(p.b0 + g / per) * kBetaSamples + s_lo + g % per) * ntri);
-          v[u] = src[c];
-        }
+      for (int u = 0; u < kU; ++u) {
+        const int i = min(i0 + int(threadIdx.x) + u * int(blockDim.x), nq * n4 - 1);
+        const int j = i / n4, g = min(q0 + j, total - 1);
+        const float4* src = reinterpret_cast<const float4*>(
+            p.bkred + (size_t(p.b0 + g / per) * kBetaSamples + s_lo + g % per) * ntri);
+        v[u] = src[i - j * n4];
+      }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int j = j0 + (threadIdx.x >> 6) + W * u;
-          if (j < nq && c0 + lane < n4) kl4[j * n4 + c] = v[u];
-        }
+      for (int u = 0; u < kU; ++u) {
+        const int i = i0 + int(threadIdx.x) + u * int(blockDim.x);
+        if (i < nq * n4) kl4[i] = v[u];
       }
     }
     __syncthreads();

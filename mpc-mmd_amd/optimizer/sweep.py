@@ -160,6 +160,21 @@ def run_block_concurrent(prob, handles, cost, ids, init_state, mean, cov, v_des=
     return np.stack(rows) if rows else np.zeros((0, row_width(prob.num_reduced)), np.float32)
 
 
+def batch_handle(prob, G):
+    """A batch handle for up to ``G`` configurations, halving ``G`` while the
+    device refuses the buffers (the mmd_opt buffers grow with G * B * M^2:
+    n = 50 at B = 100 is ~25 MB per candidate).  A failed create frees what it
+    allocated (mpcmmd_create_batch), so retrying in this process is safe."""
+    from . import _native
+    while True:
+        try:
+            return _native.Handle(prob._cfg, max_configs=G)
+        except _native.NativeError:
+            if G <= 1:
+                raise
+            G //= 2
+
+
 def run_block_batch(prob, handle, cost, ids, init_state, mean, cov, v_des=15.0, variant="static"):
     """Solve configs ``ids`` with handle.max_configs configurations per
     batch (mpcmmd_solve_batch: every kernel is one launch over
@@ -239,7 +254,7 @@ def main():
     if a.batch > 0:
         from . import _native
         G = max(1, min(a.batch, len(ids), 65535 // a.num_batch))
-        hb = _native.Handle(prob._cfg, max_configs=G)
+        hb = batch_handle(prob, G)
         rows = run_block_batch(prob, hb, a.cost, ids, init, mean, cov, variant=a.variant)
         hb.close()
     elif a.streams > 1:
