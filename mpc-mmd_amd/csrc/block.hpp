@@ -84,7 +84,7 @@ struct ReduceScratch {
   int list_n;
   float v_lo, v_hi;
   unsigned long long t0;
-  unsigned long long gm[128];  // 8-lane group maxima of block_cvar (blockDim <= 1024)
+  alignas(16) unsigned long long gm[128];  // 8-lane group maxima of block_cvar (blockDim <= 1024)
 };
 
 // largest 64-bit word over each group of 8 lanes (quad butterflies, then
@@ -135,8 +135,13 @@ DEVI float block_cvar(const float* vals, int S, unsigned long long* list, Reduce
   __syncthreads();
   if (need <= G && tid < G) {
     const unsigned long long g = rs.gm[tid];
+    const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(rs.gm);
     int r = 0;
-    for (int q = 0; q < G; ++q) r += rs.gm[q] > g;  // LDS broadcast reads
+#pragma unroll 8
+    for (int q = 0; q < (G >> 1); ++q) {  // LDS broadcast reads, several in flight (G even)
+      const ulonglong2 v = g2[q];
+      r += int(v.x > g) + int(v.y > g);
+    }
     if (r == need - 1) rs.t0 = g;  // empty groups (0) share a rank: any of them writes 0
   }
   __syncthreads();
@@ -150,7 +155,8 @@ DEVI float block_cvar(const float* vals, int S, unsigned long long* list, Reduce
   for (int a = tid; a < c; a += blockDim.x) {
     const unsigned long long ka = list[a];
     int r = 0;  // words above ka: its position from the top
-    for (int q = 0; q < c; ++q) r += list[q] > ka;
+#pragma unroll 8
+    for (int q = 0; q < c; ++q) r += list[q] > ka;  // several broadcast reads in flight
     const int ia = int(ka & 0xFFFFFFFFull);
     if (r == S - 1 - lo) rs.v_lo = vals[ia];
     if (r == S - 1 - hi) rs.v_hi = vals[ia];
