@@ -242,17 +242,12 @@ constexpr int kMomRowsPerBlock = 4;
 constexpr double kSeriesAMaxRow = 1.0;                     // == kSeriesAMax (k_bkernel)
 constexpr float kNegLog2eRow = -1.44269504088896340736f;   // == kNegLog2e
 
+// one distance row (global row index gw over the launch's candidates) held in x
 template <int NV4>
-__global__ __launch_bounds__(64 * kMomRowsPerBlock) void k_bmoment(Params p) {
+DEVI void bmoment_row(const Params& p, int gw, const float4 (&x)[NV4]) {
   const int lane = threadIdx.x & 63;
-  const int gw = blockIdx.x * kMomRowsPerBlock + (threadIdx.x >> 6);
-  const int M = p.M, Md = dist_stride(M);
-  if (gw >= p.Bt * M) return;  // wave-uniform
+  const int M = p.M;
   const int b = gw / M, r = gw - b * M;
-  const float4* row = reinterpret_cast<const float4*>(p.bdist + (size_t(b) * M + r) * Md) + lane;
-  float4 x[NV4];
-#pragma unroll
-  for (int t = 0; t < NV4; ++t) x[t] = row[64 * t];
   // columns j = 4 (lane + 64 t) + c; pad columns j >= M
   auto valid = [&](int t, int c) { return 4 * (lane + 64 * t) + c < M; };
   float mx = 0.0f;
@@ -320,6 +315,37 @@ __global__ __launch_bounds__(64 * kMomRowsPerBlock) void k_bmoment(Params p) {
       const float sum = wave_total(acc2.x + acc2.y);
       if (lane == 0) rowsum[i] = sum;
     }
+  }
+}
+
+// rows per wave: the next row's loads are issued before the current row is
+// processed (a wave no longer waits one full memory latency per row)
+template <int NV4>
+constexpr int mom_rows_per_wave() { return NV4 <= 2 ? 4 : (NV4 <= 4 ? 2 : 1); }
+
+template <int NV4>
+__global__ __launch_bounds__(64 * kMomRowsPerBlock) void k_bmoment(Params p) {
+  constexpr int RPW = mom_rows_per_wave<NV4>();
+  const int lane = threadIdx.x & 63;
+  const int total = p.Bt * p.M, Md = dist_stride(p.M);
+  const int g0 = (blockIdx.x * kMomRowsPerBlock + (threadIdx.x >> 6)) * RPW;
+  if (g0 >= total) return;  // wave-uniform
+  auto load = [&](float4 (&x)[NV4], int g) {
+    const float4* row = reinterpret_cast<const float4*>(p.bdist + size_t(g) * Md) + lane;  // rows of all candidates are consecutive
+#pragma unroll
+    for (int t = 0; t < NV4; ++t) x[t] = row[64 * t];
+  };
+  float4 x[NV4], xn[NV4];
+  load(x, g0);
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int g = g0 + i;
+    if (g >= total) break;  // wave-uniform
+    if (i + 1 < RPW) load(xn, min(g + 1, total - 1));
+    bmoment_row<NV4>(p, g, x);
+    if (i + 1 < RPW)
+#pragma unroll
+      for (int t = 0; t < NV4; ++t) x[t] = xn[t];
   }
 }
 
@@ -2215,8 +2241,8 @@ void launch_bdist(const Params& p, hipStream_t s) {
 
 template <int NV4>
 void launch_bmoment_v(const Params& p, hipStream_t s) {
-  const size_t rows = size_t(p.Bt) * p.M;
-  hipLaunchKernelGGL((k_bmoment<NV4>), dim3((rows + kMomRowsPerBlock - 1) / kMomRowsPerBlock),
+  const size_t rows = size_t(p.Bt) * p.M, per = size_t(kMomRowsPerBlock) * mom_rows_per_wave<NV4>();
+  hipLaunchKernelGGL((k_bmoment<NV4>), dim3((rows + per - 1) / per),
                      dim3(64 * kMomRowsPerBlock), 0, s, p);
 }
 
