@@ -654,11 +654,11 @@ struct SampleBlock {
   double uX[3];  // U[p0 + r][4i + h]        (B of W U^T, A of U S)
   double L;      // L_jj of position p0 + r
   double m[4];   // mean of position p0 + h + 4i
-  double z[TPW][4];  // Z[p0 + 4k + h][sample of (tile t, lane r)] (sample_of)
+  float z[TPW][4];   // Z[p0 + 4k + h][sample of (tile t, lane r)] (sample_of); fp32 normals, widened at use
 };
 
 template <int TPW>
-DEVI void load_block(SampleBlock<TPW>& q, const double* G, const double* gm, const double* z, int p0, int s0, int r,
+DEVI void load_block(SampleBlock<TPW>& q, const double* G, const double* gm, const float* z, int p0, int s0, int r,
                      int h) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) q.wA[k] = G[size_t(p0 + 4 * k + h) * kGenStride + kGenW + r];  // rows >= 11 of S unused
@@ -682,8 +682,8 @@ DEVI void load_block(SampleBlock<TPW>& q, const double* G, const double* gm, con
     for (int u = 0; u < TPW / 2; ++u)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const double2 zz =
-            *reinterpret_cast<const double2*>(z + size_t(p0 + 4 * k + h) * kBzCols + s0 + 32 * u + 2 * r);
+        const float2 zz =
+            *reinterpret_cast<const float2*>(z + size_t(p0 + 4 * k + h) * kBzCols + s0 + 32 * u + 2 * r);
         q.z[2 * u][k] = zz.x;
         q.z[2 * u + 1][k] = zz.y;
       }
@@ -699,6 +699,11 @@ DEVI void load_block(SampleBlock<TPW>& q, const double* G, const double* gm, con
 // for a vector add between blocks.
 template <int TPW>
 DEVI void block_mfma(const SampleBlock<TPW>& cur, d4* S, const d4* Sp, d4* Y, int r, int h) {
+  double zd[TPW][4];  // the fp32 normals widened once (exact), used by two MFMA chains
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) zd[t][k] = double(cur.z[t][k]);
   d4 X = d4{0.0, 0.0, 0.0, 0.0};  // X = W_c U_c^T: register i holds w_{h+4i} . u_r = T[row r][col h + 4i]
 #pragma unroll
   for (int i = 0; i < 3; ++i) X = mfma64(cur.wX[i], cur.uX[i], X);
@@ -716,7 +721,7 @@ DEVI void block_mfma(const SampleBlock<TPW>& cur, d4* S, const d4* Sp, d4* Y, in
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) S[t] = mfma64(cur.wA[k], cur.z[t][k], S[t]);
+    for (int t = 0; t < TPW; ++t) S[t] = mfma64(cur.wA[k], zd[t][k], S[t]);
   double T[4];  // A operand of T Z, k-step i: T[r][4i + h]
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -726,7 +731,7 @@ DEVI void block_mfma(const SampleBlock<TPW>& cur, d4* S, const d4* Sp, d4* Y, in
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) Y[t] = mfma64(T[k], cur.z[t][k], Y[t]);
+    for (int t = 0; t < TPW; ++t) Y[t] = mfma64(T[k], zd[t][k], Y[t]);
 }
 
 // the finished block's samples to fp32 (the sigma coordinate M clipped)
@@ -767,7 +772,7 @@ __global__ __launch_bounds__(64 * sample_waves<TPW>()) void k_bsample(Params p, 
   MPCMMD_STAMP(p, 0);
   const double* G = p.gen + size_t(b) * Pp * kGenStride;
   const double* gm = p.genm + size_t(b) * Pp;
-  const double* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
+  const float* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
   const int ys = ygen_stride(M);
   float* Y = p.ygen + (size_t(b) * kBzCols + s0 + (TPW == 1 ? r : 2 * r)) * ys;
   d4 S[TPW], Sp[TPW], Ya[TPW], Yb[TPW];
@@ -816,7 +821,7 @@ __global__ __launch_bounds__(64 * kChunkWavesMax) void k_bsample_chunks(Params p
   MPCMMD_STAMP(p, 0);
   const double* G = p.gen + size_t(b) * Pp * kGenStride;
   const double* gm = p.genm + size_t(b) * Pp;
-  const double* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
+  const float* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
   const int ys = ygen_stride(M);
   float* Y = p.ygen + (size_t(b) * kBzCols + s0 + r) * ys;
   if (k < P - 1) {
@@ -826,7 +831,7 @@ __global__ __launch_bounds__(64 * kChunkWavesMax) void k_bsample_chunks(Params p
       for (int kk = 0; kk < 4; ++kk) {
         const size_t pos = size_t(c) * 16 + 4 * kk + h;
         wa[kk] = G[pos * kGenStride + kGenW + r];
-        zz[kk] = z[pos * kBzCols + s0 + r];
+        zz[kk] = double(z[pos * kBzCols + s0 + r]);
       }
     };
     d4 Sl = d4{0.0, 0.0, 0.0, 0.0};
@@ -2127,13 +2132,13 @@ __global__ __launch_bounds__(kThreads) void k_bsigma(Params p, int tb) {
   if (imin < kBetaElite) return;  // k_belite wrote it
   const double* gen = p.gen + size_t(b) * pos_pad(M) * kGenStride;
   {
-    const double* z = p.beta_z + size_t(tb) * pos_pad(M) * kBzCols;
+    const float* z = p.beta_z + size_t(tb) * pos_pad(M) * kBzCols;
     const int si = imin - kBetaElite;
     double part[11];
 #pragma unroll
     for (int a = 0; a < 11; ++a) part[a] = 0.0;
     for (int j = tid; j < M; j += blockDim.x) {
-      const double zj = z[size_t(j) * kBzCols + si];
+      const double zj = double(z[size_t(j) * kBzCols + si]);
 #pragma unroll
       for (int a = 0; a < 11; ++a) part[a] += gen[size_t(j) * kGenStride + kGenW + a] * zj;
     }

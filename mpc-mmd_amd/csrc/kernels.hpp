@@ -80,7 +80,7 @@ struct Params {
   uint32_t* bfix_n;        // their count (zeroed by k_gamma_tab)
   double* gtab;            // [G][gamma_tab_size] Beta-noise attempt tables of the current iteration
   const float* beta_z0;    // [100][M+1]
-  const double* beta_z;    // [20][pos_pad(M)][kBzCols] fp32 normals held as fp64 (position-major, zero padded)
+  const float* beta_z;     // [20][pos_pad(M)][kBzCols] fp32 normals (position-major, zero padded)
   // carry / state
   float* pop;              // [2][Bt][8] double-buffered population
   float* mean;             // [G][8]

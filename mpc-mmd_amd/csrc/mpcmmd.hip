@@ -220,10 +220,10 @@ size_t stage_size(int B, int S, int H, int O, int T, int G) {
 // for 16 samples in one transaction and whole 16 x 16 blocks without bounds
 void upload_beta_z(mpcmmd_handle* h, int t, const float* z) {
   const int M1 = h->M + 1, R = kBetaSamples - kBetaElite;
-  std::vector<double> tr(size_t(pos_pad(h->M)) * kBzCols, 0.0);
+  std::vector<float> tr(size_t(pos_pad(h->M)) * kBzCols, 0.0f);
   for (int r = 0; r < R; ++r)
-    for (int j = 0; j < M1; ++j) tr[size_t(j) * kBzCols + r] = double(z[size_t(r) * M1 + j]);
-  upload(h, "beta_z", tr.data(), tr.size() * 8, size_t(t) * tr.size() * 8);
+    for (int j = 0; j < M1; ++j) tr[size_t(j) * kBzCols + r] = z[size_t(r) * M1 + j];
+  upload(h, "beta_z", tr.data(), tr.size() * 4, size_t(t) * tr.size() * 4);
   HIPC(hipStreamSynchronize(h->stream));  // tr is a host temporary
 }
 
@@ -513,7 +513,7 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     p.gtab = c.noise == MPCMMD_NOISE_BETA ? (double*)h->alloc("gtab", size_t(GM) * gamma_tab_size(S, H) * 8) : nullptr;
     if (mmd_ok) {
       p.beta_z0 = (const float*)h->alloc("beta_z0", size_t(kBetaSamples) * (h->M + 1) * 4);
-      p.beta_z = (const double*)h->alloc("beta_z", size_t(kBetaIters) * pos_pad(h->M) * kBzCols * 8);
+      p.beta_z = (const float*)h->alloc("beta_z", size_t(kBetaIters) * pos_pad(h->M) * kBzCols * 4);
       const size_t M = h->M, M1 = M + 1, n = h->n;
       p.feat = (float*)h->alloc("feat", BT * 22 * M * 4);
       p.featr = (float*)h->alloc("featr", BT * M * kFeatStride * 4);
