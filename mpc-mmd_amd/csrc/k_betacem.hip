@@ -1961,12 +1961,7 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
       const double m = s / double(kBetaElite);
 #pragma unroll
       for (int q = 0; q < kBetaElite; ++q) u[q] = valid ? (double(v[q]) - m) * rs10 : 0.0;
-      if (valid) {
-        double* gj = gen + size_t(j) * kGenStride + kGenU;
-#pragma unroll
-        for (int q = 0; q < kBetaElite; ++q) gj[q] = u[q];
-        p.genm[size_t(b) * pos_pad(M) + j] = double(float(m));
-      }
+      if (valid) p.genm[size_t(b) * pos_pad(M) + j] = double(float(m));
     }
     // level 1: block sums G = U^T U of u u^T over each 16-position block (66
     // packed entries) on fp64 MFMA: the wave's four blocks one at a time, the
@@ -1989,6 +1984,15 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
       for (int st = 0; st < 4; ++st) {
         const double x = r < 11 ? ub[(4 * st + h) * kUPitch + r] : 0.0;
         G = mfma64(x, x, G);
+      }
+      // the block's u rows into gen from the same staging: consecutive lanes
+      // on consecutive features of a row, so a store instruction covers ~6
+      // position rows (a lane per position wrote 64 rows per instruction)
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int e = lane + 64 * i, row = e / kBetaElite, q = e - row * kBetaElite;
+        const int pos = blk * 16 + row;
+        if (e < 16 * kBetaElite && pos < M1) gen[size_t(pos) * kGenStride + kGenU + q] = ub[row * kUPitch + q];
       }
       wave_sync();
       // register i: G[h + 4 i][r]; the packed upper triangle a <= c
