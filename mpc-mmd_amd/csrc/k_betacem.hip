@@ -658,15 +658,16 @@ struct SampleBlock {
 };
 
 template <int TPW>
-DEVI void load_block(SampleBlock<TPW>& q, const double* G, const double* gm, const float* z, int p0, int s0, int r,
-                     int h) {
+DEVI void load_block(SampleBlock<TPW>& q, const double* G, const double* GU, const double* gm, const float* z, int p0,
+                     int s0, int r, int h) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) q.wA[k] = G[size_t(p0 + 4 * k + h) * kGenStride + kGenW + r];  // rows >= 11 of S unused
-  const double* g = G + size_t(p0 + r) * kGenStride;
+  for (int k = 0; k < 4; ++k) q.wA[k] = G[size_t(p0 + 4 * k + h) * kGenRow + kGenW + r];  // rows > 11 of S unused
+  const double* g = G + size_t(p0 + r) * kGenRow;
+  const double* gu = GU + size_t(p0 + r) * kGenRow;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    q.wX[i] = g[kGenW + 4 * i + h];  // feature 11 reads a zero slot
-    q.uX[i] = g[kGenU + 4 * i + h];
+    q.wX[i] = g[kGenW + 4 * i + h];  // feature 11 reads L_jj, times U's zero feature 11
+    q.uX[i] = gu[4 * i + h];
   }
   q.L = g[kGenL];
 #pragma unroll
@@ -739,8 +740,11 @@ DEVI void block_mfma(const SampleBlock<TPW>& cur, d4* S, const d4* Sp, d4* Y, in
 // across (lane row, register) -- a block swap by permlane32, then the 2 x 2
 // blocks by permlane16 -- leaves positions p0 + 4h .. p0 + 4h + 3 in lane row
 // h, stored as one 16-byte write per tile.
+// Blocks wholly past the sigma coordinate and the padding samples >= kNew of
+// the last tile are not stored (k_bselect never reads them).
 template <int TPW>
-DEVI void block_store(const d4* Yv, float* Y, int p0, int M, int ys, int h) {
+DEVI void block_store(const d4* Yv, float* Y, int p0, int M, int ys, int sl, int h) {
+  if (p0 > M) return;
 #pragma unroll
   for (int t = 0; t < TPW; ++t) {
     float v[4];
@@ -751,8 +755,9 @@ DEVI void block_store(const d4* Yv, float* Y, int p0, int M, int ys, int h) {
     permlane_swap<16>(v[0], v[1]);
     permlane_swap<16>(v[2], v[3]);
     // sample s0 + 32 (t / 2) + 2 r + t % 2 (one tile per wave: s0 + r)
-    float4* yrow = reinterpret_cast<float4*>(Y + size_t(TPW == 1 ? 0 : 32 * (t >> 1) + (t & 1)) * ys + p0 + 4 * h);
-    *yrow = make_float4(v[0], v[1], v[2], v[3]);
+    const int so = TPW == 1 ? 0 : 32 * (t >> 1) + (t & 1);
+    float4* yrow = reinterpret_cast<float4*>(Y + size_t(so) * ys + p0 + 4 * h);
+    if (sl + so < kNew) *yrow = make_float4(v[0], v[1], v[2], v[3]);  // sl: the lane's sample of tile 0
   }
 }
 
@@ -774,7 +779,8 @@ __global__ __launch_bounds__(64 * sample_waves<TPW>()) void k_bsample(Params p, 
   const double* gm = p.genm + size_t(b) * Pp;
   const float* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
   const int ys = ygen_stride(M);
-  float* Y = p.ygen + (size_t(b) * kBzCols + s0 + (TPW == 1 ? r : 2 * r)) * ys;
+  const int sl = s0 + (TPW == 1 ? r : 2 * r);
+  float* Y = p.ygen + (size_t(b) * kBzCols + sl) * ys;
   d4 S[TPW], Sp[TPW], Ya[TPW], Yb[TPW];
 #pragma unroll
   for (int t = 0; t < TPW; ++t) S[t] = Sp[t] = d4{0.0, 0.0, 0.0, 0.0};
@@ -784,26 +790,26 @@ __global__ __launch_bounds__(64 * sample_waves<TPW>()) void k_bsample(Params p, 
   // are converted and stored (the last prefetch re-reads a block; nblk and
   // the chunk length are even; sched barriers keep that order)
   SampleBlock<TPW> qa, qb;
-  load_block(qa, G, gm, z, 0, s0, r, h);
+  load_block(qa, G, G + gen_uplane(Pp), gm, z, 0, s0, r, h);
   for (int c = 0; c < nblk; c += 2) {
     const int p0 = c << 4;
-    load_block(qb, G, gm, z, p0 + 16, s0, r, h);
+    load_block(qb, G, G + gen_uplane(Pp), gm, z, p0 + 16, s0, r, h);
     __builtin_amdgcn_sched_barrier(0);
     block_mfma(qa, S, Sp, Ya, r, h);
     __builtin_amdgcn_sched_barrier(0);
-    if (c > 0) block_store<TPW>(Yb, Y, p0 - 16, M, ys, h);
+    if (c > 0) block_store<TPW>(Yb, Y, p0 - 16, M, ys, sl, h);
     __builtin_amdgcn_sched_barrier(0);
-    load_block(qa, G, gm, z, min(p0 + 32, Pp - 16), s0, r, h);
+    load_block(qa, G, G + gen_uplane(Pp), gm, z, min(p0 + 32, Pp - 16), s0, r, h);
     __builtin_amdgcn_sched_barrier(0);
     block_mfma(qb, S, Sp, Yb, r, h);
     if ((c + 2) % cl == 0)
 #pragma unroll
       for (int t = 0; t < TPW; ++t) fold_chunk(Sp[t], S[t]);
     __builtin_amdgcn_sched_barrier(0);
-    block_store<TPW>(Ya, Y, p0, M, ys, h);
+    block_store<TPW>(Ya, Y, p0, M, ys, sl, h);
     __builtin_amdgcn_sched_barrier(0);
   }
-  block_store<TPW>(Yb, Y, Pp - 16, M, ys, h);
+  block_store<TPW>(Yb, Y, Pp - 16, M, ys, sl, h);
   MPCMMD_STAMP(p, 1);
 }
 
@@ -830,7 +836,7 @@ __global__ __launch_bounds__(64 * kChunkWavesMax) void k_bsample_chunks(Params p
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         const size_t pos = size_t(c) * 16 + 4 * kk + h;
-        wa[kk] = G[pos * kGenStride + kGenW + r];
+        wa[kk] = G[pos * kGenRow + kGenW + r];
         zz[kk] = double(z[pos * kBzCols + s0 + r]);
       }
     };
@@ -857,23 +863,23 @@ __global__ __launch_bounds__(64 * kChunkWavesMax) void k_bsample_chunks(Params p
     for (int i = 0; i < 3; ++i) Sp[0][i] = Sp[0][i] + dS[j][i][lane];
   SampleBlock<1> qa, qb;
   const int pend = c1 << 4;
-  load_block(qa, G, gm, z, c0 << 4, s0, r, h);
+  load_block(qa, G, G + gen_uplane(Pp), gm, z, c0 << 4, s0, r, h);
   for (int c = c0; c < c1; c += 2) {
     const int p0 = c << 4;
-    load_block(qb, G, gm, z, p0 + 16, s0, r, h);
+    load_block(qb, G, G + gen_uplane(Pp), gm, z, p0 + 16, s0, r, h);
     __builtin_amdgcn_sched_barrier(0);
     block_mfma(qa, S, Sp, Ya, r, h);
     __builtin_amdgcn_sched_barrier(0);
-    if (c > c0) block_store<1>(Yb, Y, p0 - 16, M, ys, h);
+    if (c > c0) block_store<1>(Yb, Y, p0 - 16, M, ys, s0 + r, h);
     __builtin_amdgcn_sched_barrier(0);
-    load_block(qa, G, gm, z, min(p0 + 32, pend - 16), s0, r, h);
+    load_block(qa, G, G + gen_uplane(Pp), gm, z, min(p0 + 32, pend - 16), s0, r, h);
     __builtin_amdgcn_sched_barrier(0);
     block_mfma(qb, S, Sp, Yb, r, h);
     __builtin_amdgcn_sched_barrier(0);
-    block_store<1>(Ya, Y, p0, M, ys, h);
+    block_store<1>(Ya, Y, p0, M, ys, s0 + r, h);
     __builtin_amdgcn_sched_barrier(0);
   }
-  block_store<1>(Yb, Y, pend - 16, M, ys, h);
+  block_store<1>(Yb, Y, pend - 16, M, ys, s0 + r, h);
   MPCMMD_STAMP(p, 1);
 }
 
@@ -1992,7 +1998,7 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
       for (int i = 0; i < 3; ++i) {
         const int e = lane + 64 * i, row = e / kBetaElite, q = e - row * kBetaElite;
         const int pos = blk * 16 + row;
-        if (e < 16 * kBetaElite && pos < M1) gen[size_t(pos) * kGenStride + kGenU + q] = ub[row * kUPitch + q];
+        if (e < 16 * kBetaElite && pos < M1) gen[gen_uplane(pos_pad(M)) + size_t(pos) * kGenRow + q] = ub[row * kUPitch + q];
       }
       wave_sync();
       // register i: G[h + 4 i][r]; the packed upper triangle a <= c
@@ -2090,10 +2096,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
   }
   const int j0 = blk * 16, j1 = min(M1, j0 + 16);
-  for (int j = j0; j < j1; ++j) {
-    double u[11];  // the quad's four lanes load the same 88 bytes
+  double un[11];  // the quad's four lanes load the same 88 bytes; the next
+                  // position's u in flight while one is processed
 #pragma unroll
-    for (int c = 0; c < 11; ++c) u[c] = gen[size_t(j) * kGenStride + kGenU + c];
+  for (int c = 0; c < 11; ++c) un[c] = gen[gen_uplane(pos_pad(M)) + size_t(j0) * kGenRow + c];
+  for (int j = j0; j < j1; ++j) {
+    double u[11];
+#pragma unroll
+    for (int c = 0; c < 11; ++c) u[c] = un[c];
+    const int jn = min(j + 1, j1 - 1);
+#pragma unroll
+    for (int c = 0; c < 11; ++c) un[c] = gen[gen_uplane(pos_pad(M)) + size_t(jn) * kGenRow + c];
     double v[3], part = 0.0;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -2110,7 +2123,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     double w[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) w[i] = v[i] * rl;
-    double* g = gen + size_t(j) * kGenStride;
+    double* g = gen + size_t(j) * kGenRow;
     if (live) {
 #pragma unroll
       for (int i = 0; i < 3; ++i)
@@ -2144,7 +2157,7 @@ __global__ __launch_bounds__(kThreads) void k_bsigma(Params p, int tb) {
     for (int j = tid; j < M; j += blockDim.x) {
       const double zj = double(z[size_t(j) * kBzCols + si]);
 #pragma unroll
-      for (int a = 0; a < 11; ++a) part[a] += gen[size_t(j) * kGenStride + kGenW + a] * zj;
+      for (int a = 0; a < 11; ++a) part[a] += gen[size_t(j) * kGenRow + kGenW + a] * zj;
     }
 #pragma unroll
     for (int a = 0; a < 11; ++a) {
@@ -2156,12 +2169,13 @@ __global__ __launch_bounds__(kThreads) void k_bsigma(Params p, int tb) {
       for (int a = 0; a < 11; ++a) red[(tid >> 6) * 11 + a] = part[a];
     __syncthreads();
     if (tid == 0) {
-      const double* g = gen + size_t(M) * kGenStride;
+      const double* g = gen + size_t(M) * kGenRow;
+      const double* gu = g + gen_uplane(pos_pad(M));
       double d = 0.0;
       for (int a = 0; a < 11; ++a) {
         double sa = 0.0;
         for (int w2 = 0; w2 < (int)(blockDim.x >> 6); ++w2) sa += red[w2 * 11 + a];
-        d += g[kGenU + a] * sa;
+        d += gu[a] * sa;
       }
       const double zM = z[size_t(M) * kBzCols + si];
       const float yM = float((p.genm[size_t(b) * pos_pad(M) + M] + g[kGenL] * zM) + d);

@@ -21,8 +21,15 @@ constexpr int kResultStride = 11 + 11 + 2 + 1 + 20 + kMaxReduced;  // cx, cy, la
 // doubles per position in Params::gen: W 0..10, zeros 11..14, L_jj 15,
 // U 16..26, zeros 27..31 (the zero slots are the padding features of the
 // 16x16x4 MFMA operands, so the sampling kernel loads them unmasked)
-constexpr int kGenStride = 32;
-constexpr int kGenW = 0, kGenL = 15, kGenU = 16;
+// generators per candidate: two planes of pos_pad(M) rows x kGenRow doubles,
+// W (features 0..10, L_jj in the feature-11 slot: the sampler's K padding
+// multiplies it by U's zero feature 11) then U (features 0..10, slot 11 zero).
+// 192 B per position (the r02 row of 256 B held both with padding); planes,
+// not interleaved rows, so k_bgen's U reads and W writes never share a line.
+constexpr int kGenRow = 12;
+constexpr int kGenStride = 2 * kGenRow;  // doubles per position and candidate
+constexpr int kGenW = 0, kGenL = 11;
+HDI_CONST size_t gen_uplane(int Pp) { return size_t(Pp) * kGenRow; }  // U plane offset
 HDI_CONST int ygen_stride(int M) { return ((M + 1) + 31) & ~31; }
 // beta-CEM sample generation works on pairs of blocks of 16 positions and
 // tiles of 16 samples: generators (gen, genm) and the device normals (beta_z)
@@ -123,7 +130,7 @@ struct Params {
   float* btop;             // [B][100][n]  QP solutions
   float* bcost;            // [B][100]     QP costs
   float* belite;           // [2][B][11][M+1] elite sample vectors (ping-pong)
-  double* gen;             // [B][pos_pad(M)][kGenStride] W, L_jj, U (pad rows 0)
+  double* gen;             // [B][W, U plane][pos_pad(M)][kGenRow] (pad rows 0)
   double* phib;            // [B][ceil((M+1)/16)][66] Phi at the start of each 16-position block
   int32_t* bimin;          // [B] argmin sample of the last beta-iteration
   double* genm;            // [B][pos_pad(M)]  fp32-rounded elite mean, as fp64 (pad 0)
