@@ -673,21 +673,24 @@ DEVI void load_block(SampleBlock<TPW>& q, const double* G, const double* GU, con
 #pragma unroll
   for (int i = 0; i < 4; ++i) q.m[i] = gm[p0 + h + 4 * i];
   // tiles in pairs: lane r of tiles 2u, 2u + 1 takes samples 32u + 2r, 32u +
-  // 2r + 1, so one 16-byte load fetches both B operands (one tile per wave:
-  // lane r takes sample 16 w + r)
+  // 2r + 1 -- the lane image of bz_index, six float4 loads per block (one
+  // tile per wave: lane r takes sample s0 + r, scalar loads)
+  static_assert(TPW == 1 || TPW == kSampleTiles, "tile pairing of the normals' layout");
   if constexpr (TPW == 1) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) q.z[0][k] = z[size_t(p0 + 4 * k + h) * kBzCols + s0 + r];
+    for (int k = 0; k < 4; ++k) q.z[0][k] = z[bz_index(p0 + 4 * k + h, s0 + r)];
   } else {
+    const float4* zb = reinterpret_cast<const float4*>(z + size_t(p0 >> 4) * (16 * kBzCols)) + r + 16 * h;
 #pragma unroll
-    for (int u = 0; u < TPW / 2; ++u)
+    for (int c = 0; c < 6; ++c) {
+      const float4 f = zb[64 * c];
+      const float fv[4] = {f.x, f.y, f.z, f.w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float2 zz =
-            *reinterpret_cast<const float2*>(z + size_t(p0 + 4 * k + h) * kBzCols + s0 + 32 * u + 2 * r);
-        q.z[2 * u][k] = zz.x;
-        q.z[2 * u + 1][k] = zz.y;
+      for (int w = 0; w < 4; ++w) {
+        const int idx = 4 * c + w, k = idx / 6, t = idx % 6;  // t = 2 u + e
+        q.z[t][k] = fv[w];
       }
+    }
   }
 }
 
@@ -837,7 +840,7 @@ __global__ __launch_bounds__(64 * kChunkWavesMax) void k_bsample_chunks(Params p
       for (int kk = 0; kk < 4; ++kk) {
         const size_t pos = size_t(c) * 16 + 4 * kk + h;
         wa[kk] = G[pos * kGenRow + kGenW + r];
-        zz[kk] = double(z[pos * kBzCols + s0 + r]);
+        zz[kk] = double(z[bz_index(int(pos), s0 + r)]);
       }
     };
     d4 Sl = d4{0.0, 0.0, 0.0, 0.0};
@@ -2155,7 +2158,7 @@ __global__ __launch_bounds__(kThreads) void k_bsigma(Params p, int tb) {
 #pragma unroll
     for (int a = 0; a < 11; ++a) part[a] = 0.0;
     for (int j = tid; j < M; j += blockDim.x) {
-      const double zj = double(z[size_t(j) * kBzCols + si]);
+      const double zj = double(z[bz_index(j, si)]);
 #pragma unroll
       for (int a = 0; a < 11; ++a) part[a] += gen[size_t(j) * kGenRow + kGenW + a] * zj;
     }
@@ -2177,7 +2180,7 @@ __global__ __launch_bounds__(kThreads) void k_bsigma(Params p, int tb) {
         for (int w2 = 0; w2 < (int)(blockDim.x >> 6); ++w2) sa += red[w2 * 11 + a];
         d += gu[a] * sa;
       }
-      const double zM = z[size_t(M) * kBzCols + si];
+      const double zM = z[bz_index(M, si)];
       const float yM = float((p.genm[size_t(b) * pos_pad(M) + M] + g[kGenL] * zM) + d);
       p.sigma[b] = fmaxf(yM, 0.01f);
     }

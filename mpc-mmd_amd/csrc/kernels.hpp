@@ -36,7 +36,15 @@ HDI_CONST int ygen_stride(int M) { return ((M + 1) + 31) & ~31; }
 // are padded with zeros to pos_pad(M) positions, beta_z rows and ygen to
 // kBzCols samples
 constexpr int kBzCols = 96;
-HDI_CONST int pos_pad(int M) { return ((M + 1) + 31) & ~31; }  // whole pairs of 16-blocks
+// beta_z device layout per iteration: blocks of 16 positions x kBzCols
+// samples, each block the sampler's lane image [6 chunks][64 lanes][4 floats]:
+// lane r + 16 h holds positions p0 + 4 k + h (k < 4) of samples 32 u + 2 r + e
+// (u < 3, e < 2) at index 6 k + 2 u + e, so a wave reads a block's normals in
+// six fully coalesced float4 loads
+HDI_CONST size_t bz_index(int j, int s) {
+  const int jj = j & 15, lane = ((s & 31) >> 1) + 16 * (jj & 3), idx = 6 * (jj >> 2) + 2 * (s >> 5) + (s & 1);
+  return size_t(j >> 4) * (16 * kBzCols) + (idx >> 2) * 256 + lane * 4 + (idx & 3);
+}HDI_CONST int pos_pad(int M) { return ((M + 1) + 31) & ~31; }  // whole pairs of 16-blocks
 // row stride (floats) of the mother distance matrix: whole 256-column blocks
 // (k_bkernel: a wave holds a row as one float4 per lane and block); pad
 // columns hold +inf
@@ -87,7 +95,7 @@ struct Params {
   uint32_t* bfix_n;        // their count (zeroed by k_gamma_tab)
   double* gtab;            // [G][gamma_tab_size] Beta-noise attempt tables of the current iteration
   const float* beta_z0;    // [100][M+1]
-  const float* beta_z;     // [20][pos_pad(M)][kBzCols] fp32 normals (position-major, zero padded)
+  const float* beta_z;     // [20][pos_pad(M) * kBzCols] fp32 normals (bz_index layout, zero padded)
   // carry / state
   float* pop;              // [2][Bt][8] double-buffered population
   float* mean;             // [G][8]

@@ -215,14 +215,14 @@ size_t stage_size(int B, int S, int H, int O, int T, int G) {
   return s + 16 * 64;
 }
 
-// beta_z iteration t: [89][M+1] (draw order) -> device [pos_pad(M)][kBzCols]
-// (position-major, zero padded), so the generation kernel reads one position
-// for 16 samples in one transaction and whole 16 x 16 blocks without bounds
+// beta_z iteration t: [89][M+1] (draw order) -> device bz_index layout (the
+// sampler's lane image per 16-position block, zero padded), so the generation
+// kernel reads whole blocks without bounds in coalesced float4 loads
 void upload_beta_z(mpcmmd_handle* h, int t, const float* z) {
   const int M1 = h->M + 1, R = kBetaSamples - kBetaElite;
   std::vector<float> tr(size_t(pos_pad(h->M)) * kBzCols, 0.0f);
   for (int r = 0; r < R; ++r)
-    for (int j = 0; j < M1; ++j) tr[size_t(j) * kBzCols + r] = z[size_t(r) * M1 + j];
+    for (int j = 0; j < M1; ++j) tr[bz_index(j, r)] = z[size_t(r) * M1 + j];
   upload(h, "beta_z", tr.data(), tr.size() * 4, size_t(t) * tr.size() * 4);
   HIPC(hipStreamSynchronize(h->stream));  // tr is a host temporary
 }
