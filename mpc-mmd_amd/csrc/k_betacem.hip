@@ -242,6 +242,40 @@ constexpr int kMomRowsPerBlock = 4;
 constexpr double kSeriesAMaxRow = 1.0;                     // == kSeriesAMax (k_bkernel)
 constexpr float kNegLog2eRow = -1.44269504088896340736f;   // == kNegLog2e
 
+// wave totals of 16 per-lane values: lane l ends with the total of v[l >> 2].
+// Each butterfly step halves the values a lane carries (permlane32 / permlane16
+// swaps, then row_mirror and row_half_mirror DPP with the kept half chosen by
+// the lane bit the pairing flips, then the quad), ~35 VALU for all 16 totals
+// instead of a 7-step reduction per value.
+DEVI float wave_totals16(const float (&v)[16]) {
+  const int lane = threadIdx.x & 63;
+  float w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {  // lanes < 32 keep values 0..7, lanes >= 32 values 8..15
+    float a = v[i], b = v[i + 8];
+    permlane_swap<32>(a, b);
+    w[i] = a + b;
+  }
+  float x[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // odd rows keep the upper four
+    float a = w[i], b = w[i + 4];
+    permlane_swap<16>(a, b);
+    x[i] = a + b;
+  }
+  const bool b3 = lane & 8, b2 = lane & 4;
+  float y[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // row_mirror pairs l with l ^ 15 (bit 3 flipped)
+    const float keep = b3 ? x[i + 2] : x[i], send = b3 ? x[i] : x[i + 2];
+    y[i] = keep + __int_as_float(dpp_i<0x140>(__float_as_int(send)));
+  }
+  // row_half_mirror pairs l with l ^ 7 (bit 2 flipped)
+  float z = (b2 ? y[1] : y[0]) + __int_as_float(dpp_i<0x141>(__float_as_int(b2 ? y[0] : y[1])));
+  z += __int_as_float(dpp_i<0xB1>(__float_as_int(z)));
+  return z + __int_as_float(dpp_i<0x4E>(__float_as_int(z)));
+}
+
 // one distance row (global row index gw over the launch's candidates) held in x
 template <int NV4>
 DEVI void bmoment_row(const Params& p, int gw, const float4 (&x)[NV4]) {
@@ -279,15 +313,15 @@ DEVI void bmoment_row(const Params& p, int gw, const float4 (&x)[NV4]) {
       }
     }
   }
-  float rec = 0.0f;  // lane k < 16 ends up holding slot k of the record
+  static_assert(kMomStride == 16 && kMomR < 16 && kMom == kMomR, "record slots");
+  float v[16];  // slot k + 1 of the record: P_{k+1}
 #pragma unroll
-  for (int k = 0; k < kMom - 1; ++k) {
-    const float s = wave_total(acc[k].x + acc[k].y);
-    if (lane == k + 1) rec = s;
-  }
-  if (lane == 0) rec = float(M);
-  if (lane == kMomR) rec = R;
-  if (lane < kMomStride) p.bmom[(size_t(b) * M + r) * kMomStride + lane] = rec;
+  for (int k = 0; k < 16; ++k) v[k] = k >= 1 && k < kMom ? acc[k - 1].x + acc[k - 1].y : 0.0f;
+  const int slot = lane >> 2;  // lanes 4 s .. 4 s + 3 hold slot s
+  float rec = wave_totals16(v);
+  if (slot == 0) rec = float(M);
+  if (slot == kMomR) rec = R;
+  if ((lane & 3) == 0) p.bmom[(size_t(b) * M + r) * kMomStride + slot] = rec;
   // first-iteration pairs of this row that the series does not cover (the
   // test is k_bkernel's, on the same R and sigma)
   const int n = p.n;
