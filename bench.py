@@ -73,6 +73,10 @@ MFMA64_PEAK_TFLOPS = 78.6
 EXP_TERM_CYCLES = 8 / 64 + 2 / 128 + 2 / 128
 EXP_TERM_PEAK = SIMDS * CLOCK / EXP_TERM_CYCLES / 1e12   # 15.7 T terms/s
 HBM_PEAK_GBS = 8000.0
+# fp64 MFMA rate for the step roofline: v_mfma_f64_16x16x4 issue rate measured
+# on one SIMD by tools/microbench.hip (profiles/r04_microbench.txt), x 1024
+# SIMDs x 2.4 GHz; the guide has no fp64 MFMA figure
+MFMA64_MEASURED_TFLOPS = 78.6
 
 
 def kernel_work(w, name, launches, stats):
@@ -121,6 +125,75 @@ def kernel_work(w, name, launches, stats):
         beta = 2 * 160 if w["noise"] == "beta" else 0
         return "valu", "T lane-ops/s", launches * B * n * H * (40 + O * 9 + beta), VALU_PEAK_TOPS
     return None
+
+
+def alg_bytes_per_step(w):
+    """SURVEY §8d algorithmic HBM bytes of one step (the planes a
+    straightforward design writes once and reads once): cvar/saa/mmd_random
+    16 B S H (x, y rollout planes) + noise rows + obstacles + controls +
+    costbar + projection state (+ 16 B S H Beta planes); mmd_opt the mother
+    x, y planes and 22 fit features written and read once + projection state."""
+    B, S, H, O = w["num_batch"], w["num_reduced"], w["num_prime"], w["num_obs"]
+    state = B * (8 + 22 + 22 + 198 + 600) * 4 * 2
+    if w["cost"] == "mmd_opt":
+        M = S * S
+        return 2 * B * M * (2 * H + kF) * 4 + state + 2 * O * H * 4
+    b = 16 * B * S * H + 3 * S * H * 4 + 2 * O * H * 4 + 2 * B * H * 4 * 2 + 2 * B * S * 4 + state
+    if w["noise"] == "beta":
+        b += 16 * B * S * H
+    return b
+
+
+def step_roofline(w, busy, profile_steps, stats, ms_per_step, workload):
+    """Step-level roofline:
+    t_lower = max(bytes_alg / HBM peak, VALU lane-slots / 78.6 T/s, fp64 MFMA
+    flop / MFMA peak) per step, achieved = t_lower / measured step time,
+    hbm_frac = PMC counter bytes per step / (t x 8 TB/s) and alg_hbm_frac =
+    bytes_alg / (t x 8 TB/s) (the metric's "% HBM roofline").  VALU
+    lane-slots (fp32 lane-op equivalents; fp64 FMA and v_exp_f32 at their
+    issue cost):
+      cvar/saa/mmd_random  SURVEY §8d: B S H 36 + B S O H 9 (+ B S H 160 beta)
+      mmd_opt  this implementation's minimal work: k_bdist half matrix
+               B M (M+1)/2 22 x 2; k_bmoment B M M 11 (packed powers/adds);
+               QPs B x 89 x 20 x (n^3/6 + 4 n^2); series pairs x 28 (14 fp64
+               FMA); K_red entries x 5 (exp + scale); directly summed pairs
+               x M terms x 5
+    MFMA: k_bsample's fp64 flops (kernel_work) x launches per step, against
+    the fp64 MFMA rate measured by tools/microbench.hip
+    (profiles/r04_microbench.txt)."""
+    B, S, H, O = w["num_batch"], w["num_reduced"], w["num_prime"], w["num_obs"]
+    per = 1.0 / profile_steps
+    if w["cost"] == "mmd_opt":
+        M = S * S
+        slots = (B * M * (M + 1) / 2 * kF * 2 + B * M * M * 11 + B * 89 * 20 * (S ** 3 / 6 + 4 * S * S)
+                 + (stats[2] * 28 + stats[3] * 5 + stats[1] * M * 5) * per)
+        mflop = 0.0
+        if "bsample" in busy:
+            mflop = kernel_work(w, "bsample", busy["bsample"][0], stats)[2] * per
+    else:
+        slots = B * S * H * 36 + B * S * O * H * 9 + (B * S * H * 160 if w["noise"] == "beta" else 0)
+        mflop = 0.0
+    alg = alg_bytes_per_step(w)
+    t_hbm = alg / (HBM_PEAK_GBS * 1e9)
+    t_valu = slots / (VALU_PEAK_TOPS * 1e12)
+    t_mfma = mflop / (MFMA64_MEASURED_TFLOPS * 1e12)
+    t_lower = max(t_hbm, t_valu, t_mfma)
+    t = ms_per_step / 1e3
+    counter = 0.0
+    have = True
+    for k, (launches, _) in busy.items():
+        v = pmc_traffic(workload, k)
+        if v is None:
+            have = False
+            continue
+        counter += v * launches * per
+    bound = {t_hbm: "hbm", t_valu: "valu", t_mfma: "mfma-fp64"}[t_lower]
+    return {"t_lower_ms": t_lower * 1e3, "bound": bound, "achieved": t_lower / t, "t_hbm_ms": t_hbm * 1e3,
+            "t_valu_ms": t_valu * 1e3, "t_mfma_ms": t_mfma * 1e3, "bytes_alg": alg,
+            "alg_hbm_frac": alg / (t * HBM_PEAK_GBS * 1e9), "valu_lane_slots": slots, "mfma_flop": mflop,
+            "counter_bytes": counter if have else None,
+            "hbm_frac": counter / (t * HBM_PEAK_GBS * 1e9) if have else None,
+            "mfma_peak_tflops": MFMA64_MEASURED_TFLOPS}
 
 
 def pmc_traffic(workload, kernel):
@@ -278,6 +351,7 @@ def run_workload(name, steps, warmup, profile_steps, rank, world, local, dist=No
     if w["cost"] == "mmd_opt":  # k_bkernel work counters over the profiled pass
         roof["bkernel_counts"] = {"direct_rows": int(stats[0]), "direct_pairs": int(stats[1]),
                                   "series_pairs": int(stats[2]), "kred_entries": int(stats[3])}
+    roof["step"] = step_roofline(w, busy, profile_steps, stats, elapsed / steps * 1e3, name)
     return dict(w=w, elapsed=elapsed, step_ms=step_ms, res=res, roof=roof, inst=inst,
                 kernels={k: v[1] / profile_steps for k, v in busy.items()})
 

@@ -177,7 +177,10 @@ const char* mpcmmd_kernel_name(int32_t id);
 
 /* Named device buffers, for stage-level parity tests (read / overwrite the
  * scan carry and intermediates between stages).  Names and sizes: see
- * mpcmmd_buffer_info. */
+ * mpcmmd_buffer_info; the name "*" gives the total bytes of every buffer of
+ * the handle.  Tests can cap a handle's device memory with the environment
+ * variable MPCMMD_MAX_HANDLE_BYTES (read at create): buffers past the cap fail
+ * with the runtime's own out-of-memory error. */
 int mpcmmd_buffer_info(mpcmmd_handle* h, const char* name, size_t* bytes);
 int mpcmmd_read(mpcmmd_handle* h, const char* name, void* dst, size_t bytes);
 int mpcmmd_write(mpcmmd_handle* h, const char* name, const void* src, size_t bytes);

@@ -83,6 +83,21 @@ DEVI double row16_sum(double v) {
   return v + dpp_d<0x128>(v);
 }
 
+// Negative-control builds (tools/perturb_kred.sh): a deliberately wrong K_red
+// entry, so the parity tests can be shown to catch a kernel error.  Entry 0
+// of every sample: MPCMMD_PERTURB_KRED=1 scales it by 1.001, =2 flips its
+// mantissa bit 10 (a 1.2e-4 relative change).  Off in every product build.
+DEVI float kred_perturb(float v, int e) {
+#if defined(MPCMMD_PERTURB_KRED) && MPCMMD_PERTURB_KRED == 1
+  return e == 0 ? v * 1.001f : v;
+#elif defined(MPCMMD_PERTURB_KRED) && MPCMMD_PERTURB_KRED == 2
+  return e == 0 ? __int_as_float(__float_as_int(v) ^ (1 << 10)) : v;
+#else
+  (void)e;
+  return v;
+#endif
+}
+
 // ------------------------------------------------------------------------
 // k_mother
 __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
@@ -1301,7 +1316,8 @@ __global__ __launch_bounds__(64 * kKerWaves) __attribute__((amdgpu_waves_per_eu(
         }
 #pragma unroll
         for (int j = 0; j < kJ; ++j)
-          if (e0 + lane + 64 * j < nent) kr[e0 + lane + 64 * j] = __builtin_amdgcn_exp2f(dv[j] * cs);
+          if (e0 + lane + 64 * j < nent)
+            kr[e0 + lane + 64 * j] = kred_perturb(__builtin_amdgcn_exp2f(dv[j] * cs), e0 + lane + 64 * j);
       }
     }
   } else {
@@ -1331,7 +1347,7 @@ __global__ __launch_bounds__(64 * kKerWaves) __attribute__((amdgpu_waves_per_eu(
             dd = dd + fabsf(x.w - y.w);
           }
         }
-        kr[e] = __builtin_amdgcn_exp2f(dd * cs);
+        kr[e] = kred_perturb(__builtin_amdgcn_exp2f(dd * cs), e);
       }
       wave_sync();  // the reads are done before the next sample's rows overwrite them
     }

@@ -86,6 +86,10 @@ struct mpcmmd_handle {
   bool ext_roll = false, ext_res = false;
   bool beta_tables_internal = false;  // device beta tables hold the internal streams
   bool sel0_valid = false;            // sel0 / sig0 / rp0 / rpair0 match the device beta_z0
+  // generation of the sel0 table (bumped by every rebuild) and the one
+  // k_bmoment last used for the first beta-iteration's direct row sums: the
+  // stage API may rewrite beta_z0 between stage 4 and stage 5/6 at t = 0
+  unsigned sel0_gen = 0, bmoment_gen = ~0u;
   bool mmd_ok = false;                // mmd_opt buffers allocated (mmdopt_supported)
   std::string mmd_why;
   // pinned staging for the per-solve uploads of mpcmmd_begin: the copies are
@@ -109,10 +113,15 @@ struct mpcmmd_handle {
   int launches[kNumKernels] = {0};
   double total_ms[kNumKernels] = {0};
 
+  size_t alloc_total = 0;
+  size_t alloc_cap = 0;  // MPCMMD_MAX_HANDLE_BYTES (tests): refuse buffers past it with a real HIP OOM
   void* alloc(const std::string& name, size_t bytes) {
     void* d = nullptr;
     if (bytes == 0) bytes = 16;
-    HIPC(hipMalloc(&d, bytes));
+    alloc_total += bytes;
+    // over the cap: ask for an impossible size, so the failure is the
+    // runtime's own out-of-memory error (and its sticky last-error state)
+    HIPC(hipMalloc(&d, alloc_cap && alloc_total > alloc_cap ? (size_t(1) << 52) : bytes));
     // zeroed on the handle's own (non-blocking) stream: a null-stream memset
     // is not ordered before the constant uploads that follow on this stream
     // and could land after them
@@ -271,6 +280,15 @@ void ensure_sel0(mpcmmd_handle* h) {
   upload(h, "rpair0", pairs.data(), np * 4);
   HIPC(hipStreamSynchronize(h->stream));  // host temporaries
   h->sel0_valid = true;
+  ++h->sel0_gen;
+}
+
+// k_bmoment wrote the first beta-iteration's direct row sums for the sel0
+// table current at its launch; stages 5/6 at t = 0 rely on them
+void check_bmoment_gen(mpcmmd_handle* h) {
+  if (h->bmoment_gen != h->sel0_gen)
+    throw std::invalid_argument(
+        "beta_z0 changed (or stage 4 not run) since k_bmoment: rerun stage 4 before beta-iteration 0");
 }
 
 // one beta-CEM iteration (compute_beta.py:112-147) of candidates [p.b0, p.b0 + p.nb)
@@ -331,6 +349,7 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
         h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
         h->launch(kKBDist, [&] { launch_bdist(p, h->stream); });
         h->launch(kKBMoment, [&] { launch_bmoment(p, h->stream); });
+        h->bmoment_gen = h->sel0_gen;
         run_beta_cem(h);
         h->launch(kKMmdFinal, [&] { launch_mmdfinal(p, t, h->stream); });
       } else {
@@ -354,13 +373,18 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
         h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
         h->launch(kKBDist, [&] { launch_bdist(p, h->stream); });
         h->launch(kKBMoment, [&] { launch_bmoment(p, h->stream); });
+        h->bmoment_gen = h->sel0_gen;
       }
       if (stage == 5) {  // samples + their top-n rows
         if (t > 0) h->launch(kKBSample, [&] { launch_bsample(p, t, h->stream); });
-        if (t == 0) ensure_sel0(h);
+        if (t == 0) {
+          ensure_sel0(h);
+          check_bmoment_gen(h);
+        }
         h->launch(kKBSelect, [&] { t == 0 ? launch_bsel0(p, h->stream) : launch_bselect(p, t, h->stream); });
       }
       if (stage == 6) {  // kernel sums + QP
+        if (t == 0) check_bmoment_gen(h);
         h->launch(kKBKernel, [&] { launch_bkernel(p, t, h->stream); });
         if (t > 0) h->launch(kKBDirect, [&] { launch_bdirect(p, t, h->stream); });
         h->launch(kKBQp, [&] { launch_bqp(p, t, h->stream); });
@@ -424,6 +448,7 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
   int rc = guarded([&] {
     h->cfg = c;
     h->device = c.device;
+    if (const char* cap = std::getenv("MPCMMD_MAX_HANDLE_BYTES")) h->alloc_cap = size_t(std::strtoull(cap, nullptr, 10));
     int ndev = 0;
     HIPC(hipGetDeviceCount(&ndev));
     if (c.device < 0 || c.device >= ndev) throw std::invalid_argument("device ordinal out of range");
@@ -560,7 +585,9 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     p.res_beta = (float*)h->alloc("res_beta", BT * kBetaIters * 4);
     p.btrace = (float*)h->alloc("btrace", BT * kBetaIters * 4);
     p.dbg = (unsigned long long*)h->alloc("dbg", 64 * 8);
-    p.dbgw = (unsigned long long*)h->alloc("dbgw", size_t(65536) * 8 * 8);
+    // per-workgroup phase stamps (tools/stampsw.py) only when asked for:
+    // with dbgw null MPCMMD_STAMPW writes nothing
+    p.dbgw = std::getenv("MPCMMD_STAMPW") ? (unsigned long long*)h->alloc("dbgw", size_t(65536) * 8 * 8) : nullptr;
     p.stats = (unsigned long long*)h->alloc("stats", 8 * 8);
     p.results = (float*)h->alloc("results", size_t(GM) * T * kResultStride * 4);
     p.tr_proj = (int32_t*)h->alloc("tr_proj", size_t(GM) * T * B * 4);
@@ -591,6 +618,10 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
   });
   if (rc != MPCMMD_OK) {
     mpcmmd_destroy(h);
+    // a failed hipMalloc leaves its error as the runtime's last error; clear
+    // it so a retry in this process (optimizer/sweep.py: batch_handle halves
+    // max_configs) does not see the stale code at its first launch check
+    (void)hipGetLastError();
     return rc;
   }
   *out = h;
@@ -903,6 +934,12 @@ const char* mpcmmd_kernel_name(int32_t id) {
 
 int mpcmmd_buffer_info(mpcmmd_handle* h, const char* name, size_t* bytes) {
   if (!h || !name) return fail(MPCMMD_E_INVALID, "null argument");
+  if (std::string(name) == "*") {  // every device buffer of the handle
+    size_t tot = 0;
+    for (auto& kv : h->bufs) tot += kv.second.second;
+    if (bytes) *bytes = tot;
+    return MPCMMD_OK;
+  }
   auto it = h->bufs.find(name);
   if (it == h->bufs.end()) return fail(MPCMMD_E_INVALID, std::string("no buffer ") + name);
   if (bytes) *bytes = it->second.second;

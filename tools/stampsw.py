@@ -23,6 +23,7 @@ def main():
     w = bench.WORKLOADS[name]
     inst = bench.make_workload(w, 0)
     os.environ.setdefault("MPCMMD_GROUPS", "1")
+    os.environ["MPCMMD_STAMPW"] = "1"  # the handle allocates the stamp buffer only when asked
     cfg = _native.make_config(w["num_reduced"], w["num_obs"], w["level"], w["num_prime"], w["noise"], 0.0, 0.0,
                               num_batch=w["num_batch"], maxiter_cem=20, variant=w.get("variant", "static"))
     h = _native.Handle(cfg)
