@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define MPCMMD_ABI_VERSION 2
+#define MPCMMD_ABI_VERSION 3
 
 /* status codes */
 #define MPCMMD_OK 0
@@ -48,6 +48,12 @@ extern "C" {
  * (y_lb,y_ub at optimizer/cem.py:155; K_steer at optimizer/cem_helper.py:24) */
 #define MPCMMD_VARIANT_STATIC 0
 #define MPCMMD_VARIANT_DYNAMIC 1
+/* The CARLA optimizer (carla/optimizer/cem.py, CEM(num_reduced_sqrt,
+ * num_mother, num_obs, noise_level, num_prime, noise, town, ...)): town
+ * "Town05" / "Town10HD" select y_lb, y_ub, y_des (cem.py:161-166).  A CARLA
+ * handle solves through mpcmmd_carla_begin / mpcmmd_carla_solve only. */
+#define MPCMMD_VARIANT_CARLA_TOWN05 2
+#define MPCMMD_VARIANT_CARLA_TOWN10HD 3
 
 /* Replaces CEM.__init__(num_reduced, num_obs, noise_level, num_prime, noise,
  * acc_const_noise, steer_const_noise) (optimizer/cem.py:17-18).  num_batch is
@@ -83,6 +89,10 @@ typedef struct mpcmmd_draws {
   const float* resample;
   const float* beta_z0;
   const float* beta_z;
+  /* CARLA: [R][4] normals of the noisy initial states, R = n^2 (mmd_opt) or
+   * n (cvar) (compute_noisy_init_state(_baseline), carla/optimizer/
+   * cem_helper.py:660-715) */
+  const float* init_eps;
 } mpcmmd_draws;
 
 /* Return of compute_cem_* (cem.py:324-333 / 456-462): the obstacle-cost
@@ -102,6 +112,12 @@ typedef struct mpcmmd_result {
   int32_t* elite_proj;
   int32_t* elite_obs;
   int32_t* elite_cem;
+  /* CARLA return (carla/optimizer/cem.py:413-441): steering_best [100],
+   * v_best [100] (optional, NULL = not written), mean_param after the last
+   * iteration */
+  float* steering;
+  float* v_best;
+  float mean_param[8];
 } mpcmmd_result;
 
 typedef struct mpcmmd_handle mpcmmd_handle;
@@ -166,6 +182,51 @@ int mpcmmd_begin_batch(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const
                        const float* init_state, const float* mean, const float* cov, const float* x_obs,
                        const float* y_obs, const float* v_des);
 int mpcmmd_finish_batch(mpcmmd_handle* h, int32_t n_cfg, mpcmmd_result* out);
+
+/* ---- CARLA variant ---------------------------------------------------------
+ * The path arguments of compute_cem_mmd / compute_cem_cvar
+ * (carla/optimizer/cem.py:217-220, 444-448; main_carla.py:366-382), num_path
+ * points each (reference: 600), fp32. */
+typedef struct mpcmmd_path {
+  int32_t num_path;
+  const float* x_path;
+  const float* y_path;
+  const float* arc_vec;
+  const float* Fx_dot;
+  const float* Fy_dot;
+  const float* kappa;
+} mpcmmd_path;
+
+/* CEM.compute_cem_mmd (cost_kind MPCMMD_COST_MMD_OPT) / compute_cem_cvar
+ * (MPCMMD_COST_CVAR) of the CARLA optimizer (carla/optimizer/cem.py:217-629):
+ * init_state = init_state_global (x, y, v, vdot, psi, psidot), x_obs / y_obs
+ * the Frenet obstacle tracks [O][100], path as above.  begin then
+ * mpcmmd_iterate / mpcmmd_finish, or solve in one call.  out->steering,
+ * out->v_best, out->mean_param carry the reference's return
+ * (cx, cy, v_best, steering_best, mean_param). */
+int mpcmmd_carla_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const float init_state[6],
+                       const float mean[8], const float cov[64], const float* x_obs, const float* y_obs, float v_des,
+                       const mpcmmd_path* path, const mpcmmd_draws* draws);
+int mpcmmd_carla_solve(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const float init_state[6],
+                       const float mean[8], const float cov[64], const float* x_obs, const float* y_obs, float v_des,
+                       const mpcmmd_path* path, const mpcmmd_draws* draws, mpcmmd_result* out);
+
+/* Helper.custom_path_smoothing(x_waypoints, y_waypoints, threshold)
+ * (carla/optimizer/cem_helper.py:279-318, 391-410): 10 ADMM iterations of the
+ * jerk-smoothing QP; the (num_path+1)^2 KKT inverse is built once per
+ * num_path (fp64).  Host; no GPU needed. */
+int mpcmmd_path_smoothing(int32_t num_path, const float* x_wp, const float* y_wp, float threshold, float* x_path,
+                          float* y_path);
+/* Helper.compute_path_parameters(x_path, y_path) (cem_helper.py:321-345).
+ * Host; arc_length may be NULL. */
+int mpcmmd_path_parameters(int32_t num_path, const float* x_path, const float* y_path, float* Fx_dot, float* Fy_dot,
+                           float* Fx_ddot, float* Fy_ddot, float* arc_vec, float* kappa, float* arc_length);
+/* Helper.global_to_frenet (cem_helper.py:348-388) of count states; out
+ * [count][7] = (x, y, vx, vy, ax, ay, psi) in the Frenet frame
+ * (global_to_frenet_obs, :171-200, is this with vdot = psidot = 0 and
+ * v = |(vx, vy)|).  Host. */
+int mpcmmd_global_to_frenet(const mpcmmd_path* path, int32_t count, const float* x, const float* y, const float* v,
+                            const float* vdot, const float* psi, const float* psidot, float* out);
 
 /* Per-kernel HIP-event timing (on the handle's stream).  When enabled, every
  * launch of every kernel is bracketed by events; mpcmmd_kernel_times returns,

@@ -115,10 +115,23 @@ static std::vector<double> kkt(const std::vector<double>& cost, const std::vecto
 ProblemConsts build_constants(int num_prime, int variant) {
   ProblemConsts c;
   if (num_prime < 2 || num_prime > kNum) throw std::runtime_error("num_prime must be in [2, 100]");
+  if (variant < 0 || variant > 3) throw std::runtime_error("variant must be 0..3");
   if (variant == 1) {  // synthetic_dynamic_obs/optimizer/cem.py:155, cem_helper.py:24
     c.y_lb = -2.25;
     c.y_ub = -1.25;
     c.K_steer = 0.05;
+  }
+  if (variant >= 2) {  // carla/optimizer/cem.py:25-36, 161-166; beta steer noise sigma (2b - 1) (cem_helper.py:777)
+    c.a_obs = 4.5;
+    c.b_obs = 3.0;
+    c.wheel_base = 2.875;
+    c.K_steer = 1.0;
+    c.carla = true;
+    if (variant == 3) {  // Town10HD
+      c.y_lb = -0.3, c.y_ub = 3.8, c.y_des_1 = 0.0, c.y_des_2 = 3.5;
+    } else {  // Town05
+      c.y_lb = -3.8, c.y_ub = 0.3, c.y_des_1 = 0.0, c.y_des_2 = -3.5;
+    }
   }
   c.H = num_prime;
   // planning basis on linspace(0, 15, 100) (cem.py:42-48), cast to fp32

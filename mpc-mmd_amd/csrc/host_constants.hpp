@@ -25,6 +25,11 @@ struct ProblemConsts {
   double y_lb = -2.25, y_ub = 2.25, K_steer = 0.01;
   double alpha_mean = 0.6, alpha_cov = 0.6, lamda = 0.9;
   double ker_wt = 1000.0, alpha_quant = 0.98;
+  double y_des_1 = -1.75, y_des_2 = 1.75;
+  // CARLA variant (carla/optimizer/cem.py:29, 152-153, 182)
+  bool carla = false;
+  double a_centr = 1.5, init_mu_x = 0.3, init_mu_y = 0.0, init_sigma_x = 0.05, init_sigma_y = 0.1;
+  double gamma_lane_des = 0.3;
   int H = 0;
   // fp32-rounded basis, stored as double [100][11]
   std::vector<double> P, Pd, Pdd;
@@ -59,7 +64,7 @@ DynObsConsts build_dyn_obs_consts();
 void dyn_obs_traj(const DynObsConsts& c, int num_obs, const float* x0, const float* y0, const float* vx0,
                   const float* vy0, const float* v_des, float y_des, float* x_traj, float* y_traj);
 
-// variant: 0 static, 1 dynamic.  Throws std::runtime_error on a singular
+// variant: 0 static, 1 dynamic, 2 CARLA Town05, 3 CARLA Town10HD.  Throws std::runtime_error on a singular
 // matrix (never for valid H >= 2).
 ProblemConsts build_constants(int num_prime, int variant);
 

@@ -122,7 +122,10 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
     // jnp.repeat(acc, n, 0) / jnp.tile(steer, (n, 1)) (cem_helper.py:510-511)
     const float* ar = an + (m / n) * H;
     const float* sr = sn + (m % n) * H;
-    float x = cf.st0[0], y = cf.st0[1], vx = cf.st0[2], vy = cf.st0[3], psi = cf.st0[4];
+    // CARLA: every mother row starts from its own noisy initial state
+    // (carla/optimizer/cem.py:251-253, cem_helper.py:846)
+    const float* st = p.carla ? p.st0r + (size_t(cf.g) * p.R0 + m) * 8 : cf.st0;
+    float x = st[0], y = st[1], vx = st[2], vy = st[3], psi = st[4];
     double cx[11], cy[11];
 #pragma unroll
     for (int k = 0; k < 11; ++k) cx[k] = cy[k] = 0.0;
@@ -135,7 +138,8 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
         cy[k] = cy[k] + f * dy;
       }
       if (h == H - 1) break;
-      bicycle_step(x, y, vx, vy, psi, ar[h], sr[h]);
+      if (p.carla) bicycle_step_cr(x, y, vx, vy, psi, ar[h], sr[h], p.wheel_base);
+      else bicycle_step(x, y, vx, vy, psi, ar[h], sr[h]);
     }
     float fr[kFeatStride];
 #pragma unroll

@@ -15,6 +15,7 @@
 // GEMVs with inverses built on the host (host_constants.cpp).  Elementwise
 // work is fp32 in the reference's operation order (-ffp-contract=off).
 #include "common.hpp"
+#include "frenet.hpp"
 #include "kernels.hpp"
 
 namespace mpcmmd {
@@ -109,7 +110,17 @@ DEVI Polar polar_of(float alpha, float wx, float wy, float lo, float hi) {
 
 __global__ __launch_bounds__(256) void k_front(Params p, int t) {
   __shared__ float sB[3 * kN * kNv];
+  extern __shared__ float sPath[];  // CARLA: arc_vec [P], kappa [P] of the candidate block's configuration
   for (int i = threadIdx.x; i < 3 * kN * kNv; i += blockDim.x) sB[i] = p.basis[i];
+  if (p.carla) {
+    // every candidate of a block belongs to one configuration when B % 4 == 0
+    // (the host checks); the block's first candidate names it
+    const float* pa = p.path + size_t(min(blockIdx.x * 4, p.Bt - 1) / p.B) * 6 * kMaxPath;
+    for (int i = threadIdx.x; i < p.P; i += blockDim.x) {
+      sPath[i] = pa[2 * kMaxPath + i];
+      sPath[p.P + i] = pa[5 * kMaxPath + i];
+    }
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -281,10 +292,13 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
 
   // ---- compute_alph_d (projection.py:193-274), no unwrap (Q13) ---------------
   Polar qv[2], qa[2];
+  float alv[2], ala[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    qv[q] = polar_of(cr_atan2(yd[q], xd[q]), xd[q], yd[q], 0.1f, 30.0f);
-    qa[q] = polar_of(cr_atan2(ydd[q], xdd[q]), xdd[q], ydd[q], 0.0f, 18.0f);
+    alv[q] = cr_atan2(yd[q], xd[q]);
+    ala[q] = cr_atan2(ydd[q], xdd[q]);
+    qv[q] = polar_of(alv[q], xd[q], yd[q], 0.1f, 30.0f);
+    qa[q] = polar_of(ala[q], xdd[q], ydd[q], 0.0f, 18.0f);
   }
   float rax[2], ray[2], rvx[2], rvy[2];
   double n_acc = 0.0, n_vel = 0.0, n_lane = 0.0;
@@ -339,6 +353,25 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
     steer[q] = float(atan(double(curv * 2.5f)));
   }
 
+  // ---- CARLA (carla/optimizer/projection.py:307-315): curvature at the
+  // clipped station, steering from the projected polar forms (replaces
+  // compute_controls' steering, carla/optimizer/cem.py:307-317)
+  float kapv[2] = {0.f, 0.f};
+  if (p.carla) {
+    const int P = p.P;
+    const float* arc = sPath;
+    const float* kap = sPath + P;
+    const float hi = arc[P - 1];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float xs = x[q] != x[q] ? x[q] : fminf(fmaxf(x[q], 0.0f), hi);  // jnp.clip (NaN kept)
+      const float k = interp_jnp(xs, arc, kap, P);
+      const float curv = (qa[q].d * cr_sin(ala[q] - alv[q])) / (qv[q].d * qv[q].d);
+      steer[q] = float(atan(double((curv + (k * qv[q].ca) / (1.0f - y[q] * k)) * p.wheel_base)));
+      kapv[q] = k;
+    }
+  }
+
   // ---- stores -----------------------------------------------------------------
   float* tr = p.traj;
   const size_t plane = size_t(p.Bt) * kN;
@@ -355,6 +388,7 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
     tr[5 * plane + row + tt] = ydd[q];
     p.acc[row + tt] = accv[q];
     p.steer[row + tt] = steer[q];
+    if (p.carla) p.kappa_i[row + tt] = kapv[q];
   }
   if (lane < kNv) {
     // lane k stores component k (every lane holds all 11 in registers)
@@ -378,7 +412,7 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
 }  // namespace
 
 void launch_front(const Params& p, int t, hipStream_t s) {
-  hipLaunchKernelGGL(k_front, dim3((p.Bt + 3) / 4), dim3(256), 0, s, p, t);
+  hipLaunchKernelGGL(k_front, dim3((p.Bt + 3) / 4), dim3(256), p.carla ? size_t(2) * p.P * 4 : 0, s, p, t);
 }
 
 }  // namespace mpcmmd

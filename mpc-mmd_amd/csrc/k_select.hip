@@ -91,12 +91,24 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
     const float sv_n0 = lane < 63 ? sv_d0 : sv_f1;
     const float sa[2] = {sv_n0 - sv[0], sv_n1 - sv[1]};  // valid for t < 98
     double n_des = 0, n_st = 0, n_sv = 0, n_sa = 0, n_v = 0, n_sp = 0, n_svp = 0, n_ydd = 0, n_xdd = 0;
+    double n_des2 = 0, n_cen = 0;  // CARLA: second desired lane, centripetal penalty
+    float kap[2] = {0.f, 0.f};
+    if (p.carla) {
+      kap[0] = p.kappa_i[row + t0];
+      kap[1] = p.kappa_i[row + t1c];
+    }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int tt = q == 0 ? t0 : t1;
       if (tt >= kN) continue;
-      const double dd = double(y[q] - (-1.75f));
+      const double dd = double(y[q] - (p.carla ? p.y_des1 : -1.75f));
       n_des += dd * dd;
+      if (p.carla) {  // carla/optimizer/cem_helper.py:529-544
+        const double d2 = double(y[q] - p.y_des2);
+        n_des2 += d2 * d2;
+        const double c = double(fmaxf(0.0f, fabsf((xd[q] * xd[q]) * kap[q]) - p.a_centr));
+        n_cen += c * c;
+      }
       n_st += double(st[q]) * double(st[q]);
       const float v = sqrtf(xd[q] * xd[q] + yd[q] * yd[q]);
       const double dv = double(v - cf.v_des);
@@ -121,11 +133,23 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
     n_svp = sqrt(wave_sum(n_svp));
     n_ydd = sqrt(wave_sum(n_ydd));
     n_xdd = sqrt(wave_sum(n_xdd));
+    if (p.carla) {
+      n_des2 = sqrt(wave_sum(n_des2));
+      n_cen = sqrt(wave_sum(n_cen));
+    }
     if (lane == 0) {
       const double cobs = double(p.w_obs * p.obs_cost[e]);
       const double clane = double(p.w_lane * p.lane_cost[e]);
-      const double tot = double(p.res_norm[e]) + 0.1 * n_v + 0.1 * (n_st + n_sv + n_sa) + 0.1 * (n_sp + n_svp) +
-                         0.02 * n_ydd + 0.02 * n_xdd + 0.0 * n_des + cobs + 0.0 * clane;
+      double tot;
+      if (p.carla) {  // carla/optimizer/cem_helper.py:546-554; risk terms weighted in fp32 (cem.py:373-375)
+        const double cdes = double(p.w_des * p.lane_des[e]);
+        tot = (double(p.res_norm[e]) + 0.1 * n_v + 0.1 * (n_st + n_sv + n_sa) + 0.1 * (n_sp + n_svp) +
+               0.02 * n_ydd + 0.02 * n_xdd + 0.01 * (n_des * n_des2) + 0.1 * n_cen) +
+              cobs + clane + cdes;
+      } else {
+        tot = double(p.res_norm[e]) + 0.1 * n_v + 0.1 * (n_st + n_sv + n_sa) + 0.1 * (n_sp + n_svp) +
+              0.02 * n_ydd + 0.02 * n_xdd + 0.0 * n_des + cobs + 0.0 * clane;
+      }
       cost20[j] = float(tot);
     }
   }
@@ -223,6 +247,8 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
     for (int c = 0; c < 8; ++c) pop_next[size_t(i) * 8 + c] = row[c];
   }
   // ---- per-iteration result (cem.py:314-315) ------------------------------
+  if (p.carla && tid < kN)  // steering of the chosen elite (carla/optimizer/cem.py:398-399, 419)
+    p.res_steer[(size_t(cf.g) * p.T + t) * kN + tid] = p.steer[size_t(g0 + el[imin_s]) * kN + tid];
   if (tid < kResultStride) {
     const int e = g0 + el[imin_s];
     float* r = cf.results + size_t(t) * kResultStride;

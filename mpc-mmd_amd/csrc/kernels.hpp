@@ -59,6 +59,7 @@ constexpr int kMom = 12;
 constexpr int kMomStride = 16;
 constexpr int kMomR = 12;
 constexpr int kMaxSplit = 8;  // workgroups per candidate of the row-sum kernels
+constexpr int kMaxPath = 2048;  // CARLA path points (the reference's num_path = 600)
 
 struct Params {
   // shapes / configuration.  A launch covers G configurations of B
@@ -154,6 +155,23 @@ struct Params {
   // summed directly (M exponentials each), [2] pairs summed by the series,
   // [3] K_red entries
   unsigned long long* stats;  // [8]
+  // CARLA variant (carla/optimizer/*.py of the reference): Frenet path,
+  // one noisy initial state per rollout row, extra cost terms
+  int32_t carla;           // 0: static / dynamic constants, 1: CARLA
+  int32_t P;               // path points of the current solve
+  int32_t R0;              // noisy initial rows per configuration (n^2 mmd_opt, n cvar)
+  float wheel_base;        // carla/optimizer/cem.py:27
+  float obs_a2, obs_b2;    // a_obs^2, b_obs^2 (cem.py:26)
+  float a_centr;           // cem.py:29
+  float y_des1, y_des2;    // cem.py:161-166
+  float w_des;             // weight of the desired-lane risk (cem.py:171-173)
+  float gamma_des;         // gamma_lane_des (cem.py:182)
+  const float* path;       // [G][6][kMaxPath]: x, y, arc_vec, Fx_dot, Fy_dot, kappa
+  const float* st0r;       // [G][R0][8] noisy initial rollout states (x, y, vx, vy, psi)
+  float* kappa_i;          // [Bt][100] curvature at the projected stations (projection.py:307)
+  float* lane_des;         // [Bt] desired-lane risk (costs.py:70-100), unweighted
+  float* rxy;              // [Bt][S][2][H] rollout points: global (x, y), then Frenet (s, d) in place
+  float* res_steer;        // [G][T][100] steering of each iteration's chosen elite
   // outputs
   float* results;          // [G][T][kResultStride]
   int32_t* tr_proj;        // [G][T][B]
@@ -241,4 +259,10 @@ void launch_belite(const Params& p, int tb, hipStream_t s);
 void launch_bgen(const Params& p, int tb, hipStream_t s);  // + k_bsigma on the last beta-iteration
 void launch_mmdfinal(const Params& p, int t, hipStream_t s);
 bool mmdopt_supported(int n, int H, int O, std::string* why);
+// CARLA variant (k_carla.hip): rollouts of rows from their noisy initial
+// states (mode 0: the baseline rows of cvar; mode 1: the reduced set of
+// mmd_opt), their Frenet transforms, then the risk reducers
+void launch_roll_carla(const Params& p, int t, int mode, hipStream_t s);
+void launch_frenet(const Params& p, hipStream_t s);
+void launch_risk_carla(const Params& p, int t, int mode, hipStream_t s);
 }  // namespace mpcmmd

@@ -15,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#include "carla_host.hpp"
 #include "host_constants.hpp"
 #include "kernels.hpp"
 #include "rng.hpp"
@@ -60,11 +61,15 @@ enum KernelId {
   kKBGen,
   kKBMoment,
   kKBDirect,
+  kKRollCarla,
+  kKFrenet,
+  kKRiskCarla,
   kNumKernels
 };
 const char* kKernelNames[kNumKernels] = {"noise",   "front", "risk_baseline", "mother",   "bdist", "bsample",
                                          "bselect", "bkernel", "bqp",         "belite", "mmdfinal", "select",
-                                         "gamma_tab", "beta_planes", "bgen",    "bmoment",     "bdirect"};
+                                         "gamma_tab", "beta_planes", "bgen",    "bmoment",     "bdirect",
+                                         "roll_carla", "frenet", "risk_carla"};
 
 }  // namespace
 
@@ -91,6 +96,8 @@ struct mpcmmd_handle {
   // stage API may rewrite beta_z0 between stage 4 and stage 5/6 at t = 0
   unsigned sel0_gen = 0, bmoment_gen = ~0u;
   bool mmd_ok = false;                // mmd_opt buffers allocated (mmdopt_supported)
+  bool carla = false;                 // CARLA variant handle (mpcmmd_carla_begin)
+  int R0 = 0;                         // noisy initial rows per configuration (CARLA)
   std::string mmd_why;
   // pinned staging for the per-solve uploads of mpcmmd_begin: the copies are
   // asynchronous, so their source must outlive the call; the next begin waits
@@ -332,6 +339,16 @@ void run_beta_cem(mpcmmd_handle* h) {
   }
 }
 
+// CARLA risk (k_carla.hip): rollouts of the rows from their noisy initial
+// states (mode 0: cvar's n baseline rows; mode 1: mmd_opt's reduced set),
+// their Frenet transforms, the reducers
+void run_carla_risk(mpcmmd_handle* h, int t, int mode) {
+  const Params& p = h->p;
+  h->launch(kKRollCarla, [&] { launch_roll_carla(p, t, mode, h->stream); });
+  h->launch(kKFrenet, [&] { launch_frenet(p, h->stream); });
+  h->launch(kKRiskCarla, [&] { launch_risk_carla(p, t, mode, h->stream); });
+}
+
 void run_stage(mpcmmd_handle* h, int stage, int t) {
   const Params& p = h->p;
   switch (stage) {
@@ -351,7 +368,11 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
         h->launch(kKBMoment, [&] { launch_bmoment(p, h->stream); });
         h->bmoment_gen = h->sel0_gen;
         run_beta_cem(h);
-        h->launch(kKMmdFinal, [&] { launch_mmdfinal(p, t, h->stream); });
+        if (h->carla) run_carla_risk(h, t, 1);
+        else h->launch(kKMmdFinal, [&] { launch_mmdfinal(p, t, h->stream); });
+      } else if (h->carla) {
+        if (p.noise == MPCMMD_NOISE_BETA) h->launch(kKBetaPlanes, [&] { launch_beta_planes(p, t, h->stream); });
+        run_carla_risk(h, t, 0);
       } else {
         if (p.noise == MPCMMD_NOISE_BETA) h->launch(kKBetaPlanes, [&] { launch_beta_planes(p, t, h->stream); });
         h->launch(kKRiskBaseline, [&] { launch_risk_baseline(p, t, h->stream); });
@@ -393,7 +414,10 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
         h->launch(kKBElite, [&] { launch_belite(p, t, h->stream); });
         h->launch(kKBGen, [&] { launch_bgen(p, t, h->stream); });
       }
-      if (stage == 8) h->launch(kKMmdFinal, [&] { launch_mmdfinal(p, t, h->stream); });
+      if (stage == 8) {
+        if (h->carla) run_carla_risk(h, t, 1);
+        else h->launch(kKMmdFinal, [&] { launch_mmdfinal(p, t, h->stream); });
+      }
       break;
     default:
       throw std::invalid_argument("stage must be 0..8");
@@ -433,8 +457,7 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
   *out = nullptr;
   const mpcmmd_config& c = *cfg;
   if (c.num_reduced < 2 || c.num_obs < 1 || c.num_prime < 2 || c.num_prime > 100 || c.num_batch < 20 ||
-      c.num_batch > 4096 || c.maxiter_cem < 1 || (c.noise != 0 && c.noise != 1) ||
-      (c.variant != 0 && c.variant != 1))
+      c.num_batch > 4096 || c.maxiter_cem < 1 || (c.noise != 0 && c.noise != 1) || c.variant < 0 || c.variant > 3)
     return fail(MPCMMD_E_INVALID,
                 "config out of range (num_reduced>=2, num_obs>=1, 2<=num_prime<=100, 20<=num_batch<=4096)");
   if (c.num_reduced > 1024) return fail(MPCMMD_E_UNSUPPORTED, "num_reduced > 1024");
@@ -493,6 +516,17 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     p.K_steer = float(h->pc.K_steer * double(c.noise_level));
     p.y_lb = float(h->pc.y_lb);
     p.y_ub = float(h->pc.y_ub);
+    h->carla = h->pc.carla;
+    p.carla = h->carla ? 1 : 0;
+    p.wheel_base = float(h->pc.wheel_base);
+    p.obs_a2 = float(h->pc.a_obs * h->pc.a_obs);
+    p.obs_b2 = float(h->pc.b_obs * h->pc.b_obs);
+    p.a_centr = float(h->pc.a_centr);
+    p.y_des1 = float(h->pc.y_des_1);
+    p.y_des2 = float(h->pc.y_des_2);
+    p.gamma_des = float(h->pc.gamma_lane_des);
+    if (h->carla && max_configs != 1)
+      throw std::invalid_argument("CARLA handles solve one configuration (max_configs = 1)");
     // constants
     std::vector<float> basis(3 * kNum * kNvar);
     for (int i = 0; i < kNum * kNvar; ++i) {
@@ -566,6 +600,16 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
       p.bkred = (float*)h->alloc("bkred", BT * kBetaSamples * tri_stride(int(n)) * 4);
       p.ygen = (float*)h->alloc("ygen", BT * kBzCols * ygen_stride(h->M) * 4);
     }
+    if (h->carla) {  // path, noisy initial rows, curvature, rollout points, steering results
+      h->R0 = mmd_ok ? std::max(h->M, S) : S;
+      p.R0 = h->R0;
+      p.path = (const float*)h->alloc("path", size_t(GM) * 6 * kMaxPath * 4);
+      p.st0r = (const float*)h->alloc("st0r", size_t(GM) * h->R0 * 8 * 4);
+      p.kappa_i = (float*)h->alloc("kappa_i", BT * kNum * 4);
+      p.lane_des = (float*)h->alloc("lane_des", BT * 4);
+      p.rxy = (float*)h->alloc("rxy", BT * S * 2 * H * 4);
+      p.res_steer = (float*)h->alloc("res_steer", size_t(GM) * T * kNum * 4);
+    }
     p.pop = (float*)h->alloc("pop", size_t(2) * BT * 8 * 4);
     p.mean = (float*)h->alloc("mean", size_t(GM) * 8 * 4);
     p.cov = (float*)h->alloc("cov", size_t(GM) * 64 * 4);
@@ -606,7 +650,7 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
         HIPC(hipEventCreateWithFlags(&h->gev_done[g], hipEventDisableTiming));
       }
     }
-    h->stage_bytes = stage_size(B, S, H, O, T, GM);
+    h->stage_bytes = stage_size(B, S, H, O, T, GM) + (h->carla ? size_t(6) * kMaxPath * 4 + size_t(h->R0) * 8 * 4 + 256 : 0);
     HIPC(hipHostMalloc(reinterpret_cast<void**>(&h->stage), h->stage_bytes, hipHostMallocDefault));
     HIPC(hipEventCreateWithFlags(&h->stage_ev, hipEventDisableTiming));
     upload(h, "basis", basis.data(), basis.size() * 4);
@@ -668,13 +712,61 @@ void* mpcmmd_get_stream(mpcmmd_handle* h) { return h ? (void*)h->stream : nullpt
 
 namespace {
 
+// CARLA per-solve setup (carla/optimizer/cem.py:248-264 mmd, 476-492 cvar):
+// R noisy initial states (compute_noisy_init_state(_baseline),
+// cem_helper.py:660-715; R = n^2 for mmd_opt, n for cvar) as rollout rows, and
+// the boundary vectors from the mean of their Frenet states
+// (global_to_frenet_vmap_1, cem_helper.py:348-388).  init_state is
+// init_state_global = (x, y, v, vdot, psi, psidot) (C/main_carla.py:352).
+void carla_rows(mpcmmd_handle* h, int cost_kind, int32_t idx_mpc, const float* is, const mpcmmd_path& path,
+                const mpcmmd_draws* draws, std::vector<float>& rows, double* bx, double* by) {
+  const int R = cost_kind == MPCMMD_COST_MMD_OPT ? h->M : h->S;
+  std::vector<float> eps;
+  if (draws && draws->init_eps) eps.assign(draws->init_eps, draws->init_eps + size_t(R) * 4);
+  else eps = host_normals(uint32_t(idx_mpc), h->cfg.seed, kStreamInitEps, 0, size_t(R) * 4);
+  const float x0 = is[0], y0 = is[1], v0 = is[2], vdot = is[3], psi0 = is[4], psidot = is[5];
+  const float vx = v0 * float(std::cos(double(psi0))), vy = v0 * float(std::sin(double(psi0)));
+  const float psi = float(std::atan2(double(vy), double(vx)));
+  const float mux = float(h->pc.init_mu_x), muy = float(h->pc.init_mu_y);
+  const float sgx = float(h->pc.init_sigma_x), sgy = float(h->pc.init_sigma_y);
+  rows.assign(size_t(h->R0) * 8, 0.0f);
+  PathView pv;
+  pv.P = path.num_path, pv.x = path.x_path, pv.y = path.y_path, pv.arc = path.arc_vec;
+  pv.Fxd = path.Fx_dot, pv.Fyd = path.Fy_dot, pv.kappa = path.kappa;
+  double sum[6] = {0, 0, 0, 0, 0, 0};
+  for (int r = 0; r < R; ++r) {
+    float* o = rows.data() + size_t(r) * 8;
+    o[0] = x0 + (eps[size_t(r) * 4] * sgx + mux);
+    o[1] = y0 + (eps[size_t(r) * 4 + 1] * sgy + muy);
+    o[2] = vx;
+    o[3] = vy;
+    o[4] = psi;
+    const float v = std::sqrt(vx * vx + vy * vy);
+    const FrenetState f = global_to_frenet(pv, o[0], o[1], v, vdot, psi, psidot);
+    const float vals[6] = {f.x, f.y, f.vx, f.vy, f.ax, f.ay};
+    for (int k = 0; k < 6; ++k) sum[k] += double(vals[k]);  // sequential (the oracle's cumsum order)
+  }
+  float m[6];
+  for (int k = 0; k < 6; ++k) m[k] = float(sum[k] / double(R));
+  bx[0] = m[0], bx[1] = m[2], bx[2] = m[4];
+  by[0] = m[1], by[1] = m[3], by[2] = m[5], by[3] = 0.0;
+}
+
 // mpcmmd_begin for n configurations (arrays with a leading configuration
 // axis); external draws only for n == 1 (the parity contract)
 int begin_impl(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t* idx_mpc, const float* init_state,
                const float* mean, const float* cov, const float* x_obs, const float* y_obs, const float* v_des,
-               const mpcmmd_draws* draws) {
+               const mpcmmd_draws* draws, const mpcmmd_path* path = nullptr) {
   if (!h || !idx_mpc || !init_state || !mean || !cov || !x_obs || !y_obs || !v_des)
     return fail(MPCMMD_E_INVALID, "null argument");
+  if (h->carla != (path != nullptr))
+    return fail(MPCMMD_E_INVALID, h->carla ? "CARLA handle: use mpcmmd_carla_begin / mpcmmd_carla_solve (a path is needed)"
+                                           : "mpcmmd_carla_begin needs a handle of a CARLA variant");
+  if (h->carla && cost_kind != MPCMMD_COST_MMD_OPT && cost_kind != MPCMMD_COST_CVAR)
+    return fail(MPCMMD_E_UNSUPPORTED, "the CARLA optimizer has compute_cem_mmd (mmd_opt) and compute_cem_cvar only");
+  if (path && (path->num_path < 4 || path->num_path > kMaxPath || !path->x_path || !path->y_path || !path->arc_vec ||
+               !path->Fx_dot || !path->Fy_dot || !path->kappa))
+    return fail(MPCMMD_E_INVALID, "path: 4 <= num_path <= 2048 and six arrays");
   if (cost_kind < 0 || cost_kind > 3) return fail(MPCMMD_E_INVALID, "cost_kind must be 0..3");
   if (n_cfg < 1 || n_cfg > h->Gmax) return fail(MPCMMD_E_INVALID, "n_cfg must be 1..max_configs of the handle");
   if (draws && n_cfg > 1) return fail(MPCMMD_E_INVALID, "external draws need n_cfg == 1");
@@ -701,10 +793,16 @@ int begin_impl(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t
     p.Bt = G * B;
     p.b0 = 0;
     p.nb = p.Bt;
-    // cem.py:161-163 weights (obs, lane)
+    // cem.py:161-163 weights (obs, lane); CARLA: carla/optimizer/cem.py:171-173 (+ desired lane)
     const float w_obs[4] = {1e3f, 1e3f, 1e3f, 1e6f}, w_lane[4] = {0.f, 0.f, 0.f, 1e6f};
     p.w_obs = w_obs[cost_kind];
     p.w_lane = w_lane[cost_kind];
+    p.w_des = 0.0f;
+    if (h->carla) {
+      p.w_obs = cost_kind == MPCMMD_COST_MMD_OPT ? 0.1f : 100.0f;
+      p.w_lane = cost_kind == MPCMMD_COST_MMD_OPT ? 0.01f : 25.0f;
+      p.w_des = 0.0f;
+    }
     upload_staged(h, "idx_mpc", idx_mpc, size_t(G) * 4);
     upload_staged(h, "v_des", v_des, size_t(G) * 4);
     // sampling_param (cem_helper.py:122-150): fixed key, the same draws for every configuration
@@ -713,11 +811,13 @@ int begin_impl(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t
     else z0 = host_normals(kFixedKey0, h->cfg.seed, kStreamPop0, 0, size_t(B) * 8);
     std::vector<double> sc(size_t(G) * 4 * kNvar, 0.0);
     std::vector<float> st0(size_t(G) * 8, 0.f), ob(size_t(G) * 2 * O * H), pop(size_t(G) * B * 8);
+    std::vector<float> rows0;  // CARLA noisy initial rows [R0][8]
     for (int g = 0; g < G; ++g) {
       const float* is = init_state + size_t(g) * 6;
       // boundary vectors (cem_helper.py:152-167) and the per-solve KKT columns
-      const double bx[3] = {is[0], is[2], is[4]};
-      const double by[4] = {is[1], is[3], is[5], 0.0};
+      double bx[3] = {is[0], is[2], is[4]};
+      double by[4] = {is[1], is[3], is[5], 0.0};
+      if (h->carla) carla_rows(h, cost_kind, idx_mpc[g], is, *path, draws, rows0, bx, by);
       double* scg = sc.data() + size_t(g) * 4 * kNvar;
       for (int k = 0; k < kNvar; ++k) {
         for (int e = 0; e < 3; ++e) scg[0 * kNvar + k] += h->pc.guess_kinv_x[k * 14 + kNvar + e] * bx[e];
@@ -750,6 +850,13 @@ int begin_impl(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t
         }
     }
     upload_staged(h, "solve_c", sc.data(), sc.size() * 8);
+    if (h->carla) {
+      upload_staged(h, "st0r", rows0.data(), rows0.size() * 4);
+      const float* arrs[6] = {path->x_path, path->y_path, path->arc_vec, path->Fx_dot, path->Fy_dot, path->kappa};
+      for (int k = 0; k < 6; ++k)
+        upload_staged(h, "path", arrs[k], size_t(path->num_path) * 4, size_t(k) * kMaxPath * 4);
+      p.P = path->num_path;
+    }
     upload_staged(h, "st0", st0.data(), st0.size() * 4);
     upload_staged(h, "obs", ob.data(), ob.size() * 4);
     upload_staged(h, "pop", pop.data(), pop.size() * 4);  // iteration 0's half: [0][G B][8]
@@ -807,6 +914,22 @@ void read_result(mpcmmd_handle* h, int g, mpcmmd_result* out) {
   out->sigma = r[24];
   std::memcpy(out->res_beta, &r[25], 20 * 4);
   if (out->beta && h->cost == MPCMMD_COST_MMD_OPT) std::memcpy(out->beta, &r[45], size_t(h->n) * 4);
+  if (h->carla) {  // carla/optimizer/cem.py:413-441: cx, cy, v_best, steering_best, mean_param
+    std::vector<float> st(kNum);
+    HIPC(hipMemcpy(st.data(), h->p.res_steer + (size_t(g) * T + h->last_t) * kNum, kNum * 4, hipMemcpyDeviceToHost));
+    if (out->steering) std::memcpy(out->steering, st.data(), kNum * 4);
+    HIPC(hipMemcpy(out->mean_param, h->p.mean + size_t(g) * 8, 8 * 4, hipMemcpyDeviceToHost));
+    if (out->v_best)
+      for (int i = 0; i < kNum; ++i) {  // v = sqrt((Pdot cx)^2 + (Pdot cy)^2), fp64 sums rounded once
+        double sx = 0.0, sy = 0.0;
+        for (int k = 0; k < kNvar; ++k) {
+          sx += h->pc.Pd[i * kNvar + k] * double(out->cx[k]);
+          sy += h->pc.Pd[i * kNvar + k] * double(out->cy[k]);
+        }
+        const float xd = float(sx), yd = float(sy);
+        out->v_best[i] = std::sqrt(xd * xd + yd * yd);
+      }
+  }
   const int Tr = h->last_t + 1;
   if (out->elite_proj)
     HIPC(hipMemcpy(out->elite_proj, h->p.tr_proj + size_t(g) * T * h->B, size_t(Tr) * h->B * 4,
@@ -899,6 +1022,65 @@ int mpcmmd_solve_batch(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const
 }
 
 int32_t mpcmmd_max_configs(mpcmmd_handle* h) { return h ? h->Gmax : 0; }
+
+int mpcmmd_carla_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const float init_state[6],
+                       const float mean[8], const float cov[64], const float* x_obs, const float* y_obs, float v_des,
+                       const mpcmmd_path* path, const mpcmmd_draws* draws) {
+  if (!path) return fail(MPCMMD_E_INVALID, "null path");
+  return begin_impl(h, 1, cost_kind, &idx_mpc, init_state, mean, cov, x_obs, y_obs, &v_des, draws, path);
+}
+
+int mpcmmd_carla_solve(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const float init_state[6],
+                       const float mean[8], const float cov[64], const float* x_obs, const float* y_obs, float v_des,
+                       const mpcmmd_path* path, const mpcmmd_draws* draws, mpcmmd_result* out) {
+  int rc = mpcmmd_carla_begin(h, cost_kind, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des, path, draws);
+  if (rc) return rc;
+  rc = mpcmmd_iterate(h, 0, h->T);
+  if (rc) return rc;
+  return mpcmmd_finish(h, out);
+}
+
+int mpcmmd_path_smoothing(int32_t num_path, const float* x_wp, const float* y_wp, float threshold, float* x_path,
+                          float* y_path) {
+  if (num_path < 4 || num_path > kMaxPath || !x_wp || !y_wp || !x_path || !y_path)
+    return fail(MPCMMD_E_INVALID, "path smoothing: 4 <= num_path <= 2048, non-null arrays");
+  try {
+    path_smoothing(num_path, x_wp, y_wp, threshold, x_path, y_path);
+    return MPCMMD_OK;
+  } catch (const std::exception& e) {
+    return fail(MPCMMD_E_INVALID, e.what());
+  }
+}
+
+int mpcmmd_path_parameters(int32_t num_path, const float* x_path, const float* y_path, float* Fx_dot, float* Fy_dot,
+                           float* Fx_ddot, float* Fy_ddot, float* arc_vec, float* kappa, float* arc_length) {
+  if (num_path < 3 || !x_path || !y_path || !Fx_dot || !Fy_dot || !Fx_ddot || !Fy_ddot || !arc_vec || !kappa)
+    return fail(MPCMMD_E_INVALID, "path parameters: num_path >= 3, non-null arrays");
+  try {
+    path_parameters(num_path, x_path, y_path, Fx_dot, Fy_dot, Fx_ddot, Fy_ddot, arc_vec, kappa, arc_length);
+    return MPCMMD_OK;
+  } catch (const std::exception& e) {
+    return fail(MPCMMD_E_INVALID, e.what());
+  }
+}
+
+int mpcmmd_global_to_frenet(const mpcmmd_path* path, int32_t count, const float* x, const float* y, const float* v,
+                            const float* vdot, const float* psi, const float* psidot, float* out) {
+  if (!path || count < 0 || (count > 0 && (!x || !y || !v || !vdot || !psi || !psidot || !out)))
+    return fail(MPCMMD_E_INVALID, "null argument");
+  if (path->num_path < 2 || !path->x_path || !path->y_path || !path->arc_vec || !path->Fx_dot || !path->Fy_dot ||
+      !path->kappa)
+    return fail(MPCMMD_E_INVALID, "path: num_path >= 2 and six arrays");
+  PathView pv;
+  pv.P = path->num_path, pv.x = path->x_path, pv.y = path->y_path, pv.arc = path->arc_vec;
+  pv.Fxd = path->Fx_dot, pv.Fyd = path->Fy_dot, pv.kappa = path->kappa;
+  for (int i = 0; i < count; ++i) {
+    const FrenetState f = global_to_frenet(pv, x[i], y[i], v[i], vdot[i], psi[i], psidot[i]);
+    float* o = out + size_t(i) * 7;
+    o[0] = f.x, o[1] = f.y, o[2] = f.vx, o[3] = f.vy, o[4] = f.ax, o[5] = f.ay, o[6] = f.psi;
+  }
+  return MPCMMD_OK;
+}
 
 int mpcmmd_profile(mpcmmd_handle* h, int32_t enable) {
   if (!h) return fail(MPCMMD_E_INVALID, "null handle");
@@ -1022,6 +1204,8 @@ int mpcmmd_validate(const mpcmmd_validate_args* a) {
   const int K = a->num_cfg, O = a->num_obs, H = a->num_prime, R = a->num_rollouts;
   if (K < 0 || R < 1 || !validate_shape_ok(O, H)) return fail(MPCMMD_E_INVALID, "validate: shape out of range");
   if (a->noise != MPCMMD_NOISE_GAUSSIAN && a->noise != MPCMMD_NOISE_BETA) return fail(MPCMMD_E_INVALID, "noise");
+  if (a->variant != MPCMMD_VARIANT_STATIC && a->variant != MPCMMD_VARIANT_DYNAMIC)
+    return fail(MPCMMD_E_UNSUPPORTED, "validate: static / dynamic variants (S/validation.py, D/validation.py)");
   if (K == 0) return MPCMMD_OK;
   if (!a->cx || !a->cy || !a->init_state || !a->x_obs || !a->y_obs || !a->keys || !a->count || !a->count_lane)
     return fail(MPCMMD_E_INVALID, "null argument");

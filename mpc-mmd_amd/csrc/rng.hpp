@@ -32,6 +32,7 @@ enum Stream : uint32_t {
   kStreamPop0 = 16,
   kStreamBetaZ0 = 17,
   kStreamBetaZ = 18,
+  kStreamInitEps = 19,  // CARLA noisy initial states, key (idx_mpc, seed) (carla/optimizer/cem_helper.py:662-665)
 };
 constexpr uint32_t kFixedKey0 = 0xFFFFFFFFu;
 constexpr int kGammaMaxAttempts = 32;

@@ -95,6 +95,21 @@ DEVI void bicycle_step(float& x, float& y, float& vx, float& vy, float& psi, flo
   y = y + vy * kDt;
 }
 
+// The CARLA variant's step (carla/optimizer/cem_helper.py:732-751): wheel
+// base 2.875, true division, tan / cos / sin evaluated in fp64 and rounded
+// once (oracle/carla.py: rollout_cr), so rollouts - and the Frenet argmins
+// taken on them - are reproducible bit for bit.
+DEVI void bicycle_step_cr(float& x, float& y, float& vx, float& vy, float& psi, float an, float sn, float wb) {
+  float v = sqrtf(vx * vx + vy * vy);
+  v = v + an * kDt;
+  const float psidot = (v * float(tan(double(sn)))) / wb;
+  psi = psi + psidot * kDt;
+  vx = v * float(cos(double(psi)));
+  vy = v * float(sin(double(psi)));
+  x = x + vx * kDt;
+  y = y + vy * kDt;
+}
+
 // compute_f_bar (costs.py:50-60): ((-(dx^2))/a^2 - dy^2/b^2) + 1
 DEVI float f_bar(float x, float y, float xo, float yo) {
   constexpr float kA2 = 18.0625f, kB2 = 7.5625f;  // 4.25^2, 2.75^2 (exact in fp32)
@@ -102,4 +117,13 @@ DEVI float f_bar(float x, float y, float xo, float yo) {
   return (-div_rc(wc * wc, kA2, 1.0f / kA2) - div_rc(ws * ws, kB2, 1.0f / kB2)) + 1.0f;
 }
 
+}  // namespace mpcmmd
+
+namespace mpcmmd {
+// compute_f_bar with the CARLA ellipse (carla/optimizer/costs.py:48-57, a =
+// 4.5, b = 3): true divisions by a^2 = 20.25, b^2 = 9
+DEVI float f_bar_ab(float x, float y, float xo, float yo, float a2, float b2) {
+  const float wc = x - xo, ws = y - yo;
+  return ((-(wc * wc)) / a2 - (ws * ws) / b2) + 1.0f;
+}
 }  // namespace mpcmmd

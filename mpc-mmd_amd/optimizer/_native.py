@@ -16,9 +16,9 @@ LIB_PATH = os.environ.get("MPCMMD_LIB", os.path.join(os.path.dirname(_HERE), "li
 
 COST = {"mmd_opt": 0, "mmd_random": 1, "cvar": 2, "saa": 3}
 NOISE = {"gaussian": 0, "beta": 1}
-VARIANT = {"static": 0, "dynamic": 1}
+VARIANT = {"static": 0, "dynamic": 1, "carla_town05": 2, "carla_town10hd": 3}
 RESULT_STRIDE_BETA_MAX = 32
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 SYMBOLS = (
     "mpcmmd_abi_version", "mpcmmd_last_error", "mpcmmd_device_count", "mpcmmd_create",
@@ -27,6 +27,8 @@ SYMBOLS = (
     "mpcmmd_kernel_name", "mpcmmd_buffer_info", "mpcmmd_read", "mpcmmd_write", "mpcmmd_run_stage",
     "mpcmmd_host_constant", "mpcmmd_obs_dynamic_traj", "mpcmmd_validate", "mpcmmd_create_batch",
     "mpcmmd_max_configs", "mpcmmd_solve_batch", "mpcmmd_begin_batch", "mpcmmd_finish_batch",
+    "mpcmmd_carla_begin", "mpcmmd_carla_solve", "mpcmmd_path_smoothing", "mpcmmd_path_parameters",
+    "mpcmmd_global_to_frenet",
 )
 
 
@@ -40,14 +42,24 @@ class Config(C.Structure):
 class Draws(C.Structure):
     _fields_ = [("pop0", C.POINTER(C.c_float)), ("roll", C.POINTER(C.c_float)),
                 ("resample", C.POINTER(C.c_float)), ("beta_z0", C.POINTER(C.c_float)),
-                ("beta_z", C.POINTER(C.c_float))]
+                ("beta_z", C.POINTER(C.c_float)), ("init_eps", C.POINTER(C.c_float))]
 
 
 class Result(C.Structure):
     _fields_ = [("cx", C.c_float * 11), ("cy", C.c_float * 11), ("cost_lane", C.c_float),
                 ("cost_obs", C.c_float), ("sigma", C.c_float), ("res_beta", C.c_float * 20),
                 ("beta", C.POINTER(C.c_float)), ("elite_proj", C.POINTER(C.c_int32)),
-                ("elite_obs", C.POINTER(C.c_int32)), ("elite_cem", C.POINTER(C.c_int32))]
+                ("elite_obs", C.POINTER(C.c_int32)), ("elite_cem", C.POINTER(C.c_int32)),
+                ("steering", C.POINTER(C.c_float)), ("v_best", C.POINTER(C.c_float)),
+                ("mean_param", C.c_float * 8)]
+
+
+class Path(C.Structure):
+    _fields_ = [("num_path", C.c_int32), ("x_path", C.POINTER(C.c_float)), ("y_path", C.POINTER(C.c_float)),
+                ("arc_vec", C.POINTER(C.c_float)), ("Fx_dot", C.POINTER(C.c_float)),
+                ("Fy_dot", C.POINTER(C.c_float)), ("kappa", C.POINTER(C.c_float))]
+
+PATH_KEYS = ("x_path", "y_path", "arc_vec", "Fx_dot", "Fy_dot", "kappa")
 
 
 class ValidateArgs(C.Structure):
@@ -114,6 +126,12 @@ def lib():
     L.mpcmmd_host_constant.argtypes = [C.POINTER(Config), C.c_char_p, C.POINTER(C.c_double), C.c_size_t]
     L.mpcmmd_validate.argtypes = [C.POINTER(ValidateArgs)]
     L.mpcmmd_obs_dynamic_traj.argtypes = [C.c_int32, fp, fp, fp, fp, fp, C.c_float, fp, fp]
+    cargs = [vp, C.c_int32, C.c_int32, fp, fp, fp, fp, fp, C.c_float, C.POINTER(Path), C.POINTER(Draws)]
+    L.mpcmmd_carla_begin.argtypes = cargs
+    L.mpcmmd_carla_solve.argtypes = cargs + [C.POINTER(Result)]
+    L.mpcmmd_path_smoothing.argtypes = [C.c_int32, fp, fp, C.c_float, fp, fp]
+    L.mpcmmd_path_parameters.argtypes = [C.c_int32, fp, fp, fp, fp, fp, fp, fp, fp, fp]
+    L.mpcmmd_global_to_frenet.argtypes = [C.POINTER(Path), C.c_int32, fp, fp, fp, fp, fp, fp, fp]
     if L.mpcmmd_abi_version() != ABI_VERSION:
         raise NativeError("libmpcmmd ABI version mismatch")
     _lib = L
@@ -186,6 +204,49 @@ def _fptr(a):
     return None if a is None else a.ctypes.data_as(C.POINTER(C.c_float))
 
 
+def make_path(path):
+    """mpcmmd_path from a dict of the six arrays (PATH_KEYS); returns
+    (Path, keep) - keep holds the contiguous fp32 copies alive."""
+    keep = {k: np.ascontiguousarray(np.asarray(path[k], np.float32).reshape(-1)) for k in PATH_KEYS}
+    P = keep["x_path"].size
+    if any(v.size != P for v in keep.values()):
+        raise ValueError("path arrays differ in length")
+    return Path(P, *(_fptr(keep[k]) for k in PATH_KEYS)), keep
+
+
+def path_smoothing(x_wp, y_wp, threshold):
+    """mpcmmd_path_smoothing (Helper.custom_path_smoothing, carla/optimizer/cem_helper.py:391-410)."""
+    xw = np.ascontiguousarray(np.asarray(x_wp, np.float32).reshape(-1))
+    yw = np.ascontiguousarray(np.asarray(y_wp, np.float32).reshape(-1))
+    xo = np.empty_like(xw)
+    yo = np.empty_like(yw)
+    check(lib().mpcmmd_path_smoothing(xw.size, _fptr(xw), _fptr(yw), float(threshold), _fptr(xo), _fptr(yo)))
+    return xo, yo
+
+
+def path_parameters(x_path, y_path):
+    """mpcmmd_path_parameters (Helper.compute_path_parameters, cem_helper.py:321-345):
+    Fx_dot, Fy_dot, Fx_ddot, Fy_ddot, arc_vec, kappa, arc_length."""
+    x = np.ascontiguousarray(np.asarray(x_path, np.float32).reshape(-1))
+    y = np.ascontiguousarray(np.asarray(y_path, np.float32).reshape(-1))
+    outs = [np.empty_like(x) for _ in range(6)]
+    al = C.c_float()
+    check(lib().mpcmmd_path_parameters(x.size, _fptr(x), _fptr(y), *[_fptr(o) for o in outs], C.byref(al)))
+    return (*outs, np.float32(al.value))
+
+
+def global_to_frenet(path, x, y, v, vdot, psi, psidot):
+    """mpcmmd_global_to_frenet (Helper.global_to_frenet, cem_helper.py:348-388) of
+    arrays of states: (x, y, vx, vy, ax, ay, psi) in the Frenet frame."""
+    a = [np.ascontiguousarray(np.asarray(u, np.float32).reshape(-1)) for u in (x, y, v, vdot, psi, psidot)]
+    n = a[0].size
+    a = [np.ascontiguousarray(np.broadcast_to(u, (n,))) for u in a]
+    out = np.empty((n, 7), np.float32)
+    pth, keep = make_path(path)
+    check(lib().mpcmmd_global_to_frenet(C.byref(pth), n, *[_fptr(u) for u in a], _fptr(out)))
+    return tuple(out[:, k] for k in range(7))
+
+
 class Handle:
     """Owns one mpcmmd_handle (one device, one stream).  ``max_configs`` > 1
     sizes it for ``solve_batch`` (that many configurations per launch)."""
@@ -222,10 +283,11 @@ class Handle:
         d = None
         if draws is not None:
             keep = {}
-            for k in ("pop0", "roll", "resample", "beta_z0", "beta_z"):
+            names = ("pop0", "roll", "resample", "beta_z0", "beta_z", "init_eps")
+            for k in names:
                 a = getattr(draws, k, None)
                 keep[k] = None if a is None else np.ascontiguousarray(a, dtype=np.float32)
-            d = Draws(*(_fptr(keep[k]) for k in ("pop0", "roll", "resample", "beta_z0", "beta_z")))
+            d = Draws(*(_fptr(keep[k]) for k in names))
             ins["_draws_keep"] = keep
         ins["draws"] = d
         return ins
@@ -238,6 +300,24 @@ class Handle:
                                    _fptr(ins["mean"]), _fptr(ins["cov"]), _fptr(ins["x_obs"]),
                                    _fptr(ins["y_obs"]), float(v_des), None if d is None else C.byref(d)))
 
+    def carla_begin(self, cost, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des, path, draws=None):
+        """mpcmmd_carla_begin: compute_cem_mmd / compute_cem_cvar of the CARLA
+        optimizer (carla/optimizer/cem.py:217-629); path: dict of PATH_KEYS."""
+        ins = self._inputs(init_state, mean, cov, x_obs, y_obs, draws)
+        pth, keep = make_path(path)
+        ins["_path"] = (pth, keep)
+        self._keep = [ins]
+        d = ins["draws"]
+        check(self._L.mpcmmd_carla_begin(self._h, COST[cost], int(idx_mpc), _fptr(ins["init_state"]),
+                                         _fptr(ins["mean"]), _fptr(ins["cov"]), _fptr(ins["x_obs"]),
+                                         _fptr(ins["y_obs"]), float(v_des), C.byref(pth),
+                                         None if d is None else C.byref(d)))
+
+    def carla_solve(self, cost, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des, path, draws=None, trace=False):
+        self.carla_begin(cost, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des, path, draws)
+        self.iterate(0, self.cfg.maxiter_cem)
+        return self.finish(trace)
+
     def iterate(self, t_begin, count):
         check(self._L.mpcmmd_iterate(self._h, int(t_begin), int(count)))
 
@@ -248,6 +328,10 @@ class Handle:
         r = Result()
         beta = np.zeros(max(self.cfg.num_reduced, 1), np.float32)
         r.beta = _fptr(beta)
+        steer = np.zeros(100, np.float32)
+        vbest = np.zeros(100, np.float32)
+        r.steering = _fptr(steer)
+        r.v_best = _fptr(vbest)
         T, B = self.cfg.maxiter_cem, self.cfg.num_batch
         tr = None
         if trace:
@@ -259,6 +343,8 @@ class Handle:
         out = dict(cx=np.array(r.cx, np.float32), cy=np.array(r.cy, np.float32),
                    cost_lane=np.float32(r.cost_lane), cost_obs=np.float32(r.cost_obs),
                    sigma=np.float32(r.sigma), res_beta=np.array(r.res_beta, np.float32), beta=beta)
+        if self.cfg.variant >= 2:
+            out.update(steering=steer, v_best=vbest, mean_param=np.array(r.mean_param, np.float32))
         if tr is not None:
             out.update(tr)
         return out

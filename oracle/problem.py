@@ -103,19 +103,40 @@ class Problem:
         self.ellite_num_cost = 20
         self.num_reduced = int(num_reduced)
         self.num_mother = self.num_reduced ** 2      # cem.py:143
+        self.y_des_1, self.y_des_2 = -1.75, 1.75
+        self.carla = variant.startswith("carla")
         if variant == "static":
             self.y_lb, self.y_ub = -2.25, 2.25        # S/opt/cem.py:155
             self.K_steer = 0.01                       # S/opt/cem_helper.py:24
         elif variant == "dynamic":
             self.y_lb, self.y_ub = -2.25, -1.25       # D/opt/cem.py:155
             self.K_steer = 0.05                       # D/opt/cem_helper.py:24
+        elif variant in ("carla_town05", "carla_town10hd"):
+            # C/opt/cem.py:25-36, 152-178: CARLA constants (the optimizer of
+            # C/main_carla.py; C/ = carla/, C/opt/ = carla/optimizer/)
+            self.a_obs, self.b_obs = 4.5, 3.0          # :26
+            self.wheel_base = 2.875                    # :27
+            self.a_centr = 1.5                         # :29
+            if variant == "carla_town10hd":            # :161-166
+                self.y_lb, self.y_ub = -0.3, 3.8
+                self.y_des_1, self.y_des_2 = 0.0, 3.5
+            else:
+                self.y_lb, self.y_ub = -3.8, 0.3
+                self.y_des_1, self.y_des_2 = 0.0, -3.5
+            self.K_steer = 1.0                         # beta steer noise sigma (2b - 1) (C/opt/cem_helper.py:777)
+            self.init_mu, self.init_sigma = (0.3, 0.0), (0.05, 0.1)   # :152-153 (noisy init states)
+            self.gamma_lane_des = 0.3                  # :182
         else:
-            raise ValueError("variant must be 'static' or 'dynamic'")
-        self.y_des_1, self.y_des_2 = -1.75, 1.75
+            raise ValueError("variant must be 'static', 'dynamic', 'carla_town05' or 'carla_town10hd'")
         self.alpha_quant = 0.98
         self.weight_mmd_lane, self.weight_mmd_obs = 0.0, 1e3
         self.weight_cvar_lane, self.weight_cvar_obs = 0.0, 1e3
         self.weight_saa_lane, self.weight_saa_obs = 1e6, 1e6
+        self.weight_mmd_lane_des = self.weight_cvar_lane_des = 0.0
+        if self.carla:                                 # C/opt/cem.py:171-174
+            self.weight_mmd_lane_des, self.weight_mmd_lane, self.weight_mmd_obs = 0.0, 0.01, 0.1
+            self.weight_cvar_lane_des, self.weight_cvar_lane, self.weight_cvar_obs = 0.0, 25.0, 100.0
+            self.weight_saa_lane, self.weight_saa_obs = 1000.0, 1000.0
         self.ker_wt = 1000.0
         self.sigma_acc = float(noise_level)
         self.sigma_steer = float(noise_level)

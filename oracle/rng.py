@@ -35,6 +35,7 @@ STREAM_ROLL_ACC, STREAM_ROLL_STEER, STREAM_ROLL_CONST = 0, 1, 2
 STREAM_RESAMPLE = 3
 STREAM_GAMMA_ACC_A, STREAM_GAMMA_ACC_B, STREAM_GAMMA_STEER_A, STREAM_GAMMA_STEER_B = 4, 5, 6, 7
 STREAM_POP0, STREAM_BETA_Z0, STREAM_BETA_Z = 16, 17, 18
+STREAM_INIT_EPS = 19   # CARLA noisy initial states, key (idx_mpc, seed)
 FIXED_KEY0 = 0xFFFFFFFF
 GAMMA_MAX_ATTEMPTS = 32
 BETA_A_RATIO, BETA_B_RATIO = 2.0, 5.0   # beta_a, beta_b (S/opt/cem.py:24)

@@ -1,0 +1,98 @@
+"""CARLA variant, host side (no GPU): the library's path helpers
+(mpcmmd_path_smoothing, mpcmmd_path_parameters, mpcmmd_global_to_frenet;
+carla/optimizer/cem_helper.py:171-410 of the reference) against the oracle's
+restatement (oracle/carla.py), bit for bit; the restated jnp.interp's known
+answers; the KKT property of the smoothing solve; the replay format."""
+import importlib.util
+import os
+
+import numpy as np
+import pytest
+
+from oracle import carla as K
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+F32 = np.float32
+
+
+def _replay():
+    spec = importlib.util.spec_from_file_location("mpcmmd_carla_replay",
+                                                  os.path.join(ROOT, "mpc-mmd_amd", "carla", "replay.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.fixture(scope="module")
+def route_waypoints():
+    R = _replay()
+    rec = R.record_synthetic(ticks=201)
+    k = 200  # inside the bend: curvature on the path
+    ego = rec["ego"][k]
+    xw = (rec["waypoints"][k, 0].astype(np.float64) - float(ego[0])).astype(F32)
+    yw = (rec["waypoints"][k, 1].astype(np.float64) - float(ego[1])).astype(F32)
+    return xw, yw
+
+
+def test_interp_known_answers():
+    xp = np.array([0.0, 1.0, 2.5, 4.0], F32)
+    fp = np.array([1.0, 3.0, -2.0, 0.5], F32)
+    # grid points give fp exactly except the last (fp[P-2] + (dx/dx) df, jnp.interp's formula)
+    assert np.array_equal(K.interp(xp[:-1], xp, fp), fp[:-1])
+    assert K.interp(np.float32(4.0), xp, fp) == F32(F32(-2.0) + F32(1.0) * F32(2.5))
+    # clamped outside, linear inside
+    assert K.interp(np.float32(-1.0), xp, fp) == fp[0] and K.interp(np.float32(9.0), xp, fp) == fp[-1]
+    assert K.interp(np.float32(0.5), xp, fp) == F32(2.0)
+    np.testing.assert_allclose(K.interp(np.float32(3.25), xp, fp), -0.75, rtol=1e-6)
+
+
+def test_path_smoothing_matches_oracle_and_kkt(route_waypoints):
+    from optimizer import _native
+    xw, yw = route_waypoints
+    xs, ys = _native.path_smoothing(xw, yw, 0.1)
+    xo, yo = K.custom_path_smoothing(xw, yw, 0.1)
+    assert np.array_equal(xs, xo) and np.array_equal(ys, yo)
+    # the equality row of the KKT system: the smoothed path starts at the first waypoint
+    assert abs(float(xs[0]) - float(xw[0])) < 1e-4 and abs(float(ys[0]) - float(yw[0])) < 1e-4
+    # smoothing moves points by about the threshold at most (d <= threshold, 10 ADMM steps)
+    assert np.max(np.hypot(xs - xw, ys - yw)) < 0.2
+
+
+def test_path_parameters_and_frenet_match_oracle(route_waypoints):
+    from optimizer import _native
+    xw, yw = route_waypoints
+    xs, ys = K.custom_path_smoothing(xw, yw, 0.1)
+    lib = _native.path_parameters(xs, ys)
+    ora = K.compute_path_parameters(xs, ys)
+    for a, b in zip(lib, ora):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    path = K.make_path(xs, ys)
+    assert float(np.abs(path["kappa"][:100]).max()) > 0.02   # the bend (radius 40 m) ahead of the ego
+    rng = np.random.default_rng(3)
+    n = 2000
+    pts = [rng.uniform(-5, 120, n), rng.uniform(-10, 60, n), rng.uniform(0, 20, n), rng.uniform(-2, 2, n),
+           rng.uniform(-np.pi, np.pi, n), rng.uniform(-0.5, 0.5, n)]
+    pts = [p.astype(F32) for p in pts]
+    got = _native.global_to_frenet(path, *pts)
+    ref = K.global_to_frenet(path, *pts)
+    for g, r in zip(got, ref):
+        assert np.array_equal(g, r)
+    # a point on the path maps to (its arc length, 0)
+    s, d = K.frenet_points(path["x_path"][[50, 250]], path["y_path"][[50, 250]], path)
+    assert np.array_equal(s, path["arc_vec"][[50, 250]]) and np.all(d == 0)
+
+
+def test_replay_format_roundtrip(tmp_path):
+    R = _replay()
+    rec = R.record_synthetic(ticks=20, town="Town10HD")
+    f = tmp_path / "tick.npz"
+    R.save(f, rec)
+    back = R.load(f)
+    assert back["town"] == "Town10HD" and int(back["num_path"]) == 600
+    for k in ("ego", "waypoints", "obstacles", "route"):
+        assert np.array_equal(back[k], rec[k])
+    assert back["ego"].shape == (20, 6) and back["waypoints"].shape == (20, 2, 600)
+    # spawn offsets of carla_simulation.py:53-56 along the route, zero velocity
+    assert back["obstacles"].shape == (20, 8, 5) and np.all(back["obstacles"][:, :, 2:4] == 0)
+    ob = R.nearest_obstacles(back["obstacles"][0], back["ego"][0], 3)
+    assert ob.shape == (3, 5) and np.all(np.diff(np.hypot(ob[:, 0], ob[:, 1])) >= 0)

@@ -1,0 +1,155 @@
+"""The CARLA optimizer (BASELINE configs[4]; carla/optimizer/cem.py:217-629 of
+the reference) on the GPU against its restatement (oracle/carla.py): one
+simulator tick of compute_cem_mmd and compute_cem_cvar at H = 60 on inputs
+built from a synthetic replay tick (mpc-mmd_amd/carla/replay.py) through the
+library's own path helpers, with injected draws.
+
+Every outer iteration is checked in lockstep: per-candidate obstacle / lane /
+desired-lane risks, steering and curvature of the projection, and the three
+elite index sets (projection order, obstacle elites, cost elites) exact; the
+returned (cx, cy, v_best, steering_best, mean_param) within 1e-4.  As for the
+static mmd_opt free run (tests/test_gpu_free_run.py), a candidate whose
+beta-CEM parted from the oracle's is accepted only at the near-tie that
+explains it (tests/parity.py: beta_divergence), and must not move an elite set.
+"""
+import importlib.util
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import beta_cem as bc
+from oracle import carla as K
+from oracle import helper as Hh
+from parity import beta_near_tie, close
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CARLA = os.path.join(ROOT, "mpc-mmd_amd", "carla")
+
+
+def _replay():
+    spec = importlib.util.spec_from_file_location("mpcmmd_carla_replay", os.path.join(CARLA, "replay.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _tick(k, num_obs=3, H=60):
+    R = _replay()
+    sys.path.insert(0, CARLA)
+    try:
+        from optimizer.cem_helper import Helper
+    finally:
+        sys.path.remove(CARLA)
+    rec = R.record_synthetic(ticks=k + 1)
+    return R.tick_inputs(rec, k, Helper(num_prime=H), num_obs)
+
+
+MEAN = np.array([10.0] * 4 + [0.0] * 4, np.float32)               # main_carla.py:306-318 (v_des = 10, y = 0)
+COV = np.diag([20.0] * 4 + [100.0] * 4).astype(np.float32)
+
+
+def _beta_trace_carla(ora, st, acc, steer, draws, t):
+    """The oracle's beta-CEM of one candidate at outer iteration t (CARLA
+    mother rollouts from the noisy initial rows)."""
+    p = ora.prob
+    H = p.num_prime
+    acc_n, steer_n = Hh.noisy_controls(p, acc[None, :H], steer[None, :H], draws, t, p.num_reduced)
+    acc_m, steer_m = Hh.mother_controls(acc_n, steer_n)
+    xm, ym = K.rollout_cr(p, acc_m, steer_m, st["rows0"][None, :, :])
+    cxm, cym = Hh.compute_coeff(p, xm, ym)
+    trace = []
+    beta, res, sigma, sel = bc.compute_cem(p, cxm[0], cym[0], draws.beta_z0, draws.beta_z, trace)
+    return dict(beta=beta, res=res, sigma=sigma, sel=sel, trace=trace)
+
+
+@pytest.mark.parametrize("cost,n,B,tick,town", [("cvar", 16, 100, 60, "Town05"), ("mmd_opt", 4, 24, 60, "Town05"),
+                                                ("cvar", 12, 100, 170, "Town10HD")])
+def test_carla_tick_lockstep(native, cost, n, B, tick, town):
+    H, O, T, level = 60, 3, 20, 0.1
+    init, xo, yo, path = _tick(tick, O, H)
+    ora = K.CarlaCEM(n, 1, O, level, H, "gaussian", town, 0.0, 0.0, num_batch=B, maxiter_cem=T)
+    variant = "carla_town10hd" if town == "Town10HD" else "carla_town05"
+    nat = native.Handle(native.make_config(n, O, level, H, "gaussian", 0.0, 0.0, num_batch=B, maxiter_cem=T,
+                                           variant=variant))
+    idx = 5
+    draws = K.CarlaDraws.random(ora.prob, np.random.default_rng(7), idx_mpc=idx, with_beta_cem=(cost == "mmd_opt"))
+    trace = []
+    ref = ora.solve_carla(cost, idx, init, MEAN, COV, xo, yo, 10.0, path, draws, trace=trace)
+    nat.carla_begin(cost, idx, init, MEAN, COV, xo, yo, 10.0, path, draws)
+    # the per-solve setup: noisy initial rows and the boundary vectors they give
+    st0 = ora.init_carla(cost, init, MEAN, COV, path, draws)
+    R = st0["rows0"].shape[0]
+    assert np.array_equal(nat.read("st0r").reshape(-1, 8)[:R, :5], st0["rows0"]), "noisy initial rows differ"
+    parted = {}
+    for t in range(T):
+        nat.iterate(t, 1)
+        nat.sync()
+        tr = trace[t]
+        close(f"steer[{t}]", nat.read("steer").reshape(-1, 100)[:B], tr["steer"], rtol=0, atol=0)
+        close(f"kappa[{t}]", nat.read("kappa_i").reshape(-1, 100)[:B], tr["kappa"], rtol=0, atol=0)
+        obs_g, lane_g, des_g = nat.read("obs_cost")[:B], nat.read("lane_cost")[:B], nat.read("lane_des")[:B]
+        fl = 1e-2 if cost == "mmd_opt" else 1e-5
+        ok = np.abs(obs_g - tr["obs"]) <= fl + 1e-4 * np.abs(tr["obs"])
+        ok &= np.abs(lane_g - tr["lane"]) <= fl + 1e-4 * np.abs(tr["lane"])
+        ok &= np.abs(des_g - tr["des"]) <= fl + 1e-4 * np.abs(tr["des"])
+        if cost == "mmd_opt":
+            res_g = nat.read("res_beta").reshape(-1, 20)[:B]
+            inner = np.all(np.abs(res_g - tr["res_beta"]) <= 1e-4 * np.abs(tr["res_beta"]) + 1e-6, axis=1)
+            inner &= np.abs(nat.read("sigma")[:B] - tr["sigma"]) <= 1e-6 * np.abs(tr["sigma"])
+            if not inner.all():
+                acc = nat.read("acc").reshape(-1, 100)[:B]
+                steer = nat.read("steer").reshape(-1, 100)[:B]
+                esum_g = nat.read("btrace").reshape(-1, 20)[:B]
+                for b in np.nonzero(~inner)[0]:
+                    _, tie, detail = beta_near_tie(_beta_trace_carla(ora, st0, acc[b], steer[b], draws, t), res_g[b],
+                                                   esum_g[b])
+                    assert tie, f"iteration {t} candidate {b}: beta-CEM differs without a near-tie ({detail})"
+                    parted[(t, int(b))] = detail
+            bad = np.nonzero(~ok)[0]
+            assert all((t, int(b)) in parted for b in bad), f"iteration {t}: risks of {bad} differ, beta-CEM equal"
+        else:
+            assert ok.all(), (f"iteration {t}: candidates {np.nonzero(~ok)[0]} differ: obs {obs_g[~ok]} vs "
+                              f"{tr['obs'][~ok]}, lane {lane_g[~ok]} vs {tr['lane'][~ok]}")
+        tp = nat.read("tr_proj", np.int32).reshape(T, B)[t]
+        to = nat.read("tr_obs", np.int32).reshape(T, 20)[t]
+        tc = nat.read("tr_cem", np.int32).reshape(T, 5)[t]
+        assert np.array_equal(tp, tr["perm"]), f"iteration {t}: projection order differs"
+        assert np.array_equal(to, tr["elite_obs"]), f"iteration {t}: obstacle elites {to} vs {tr['elite_obs']}"
+        assert np.array_equal(tc, tr["elite_cem"]), f"iteration {t}: cost elites {tc} vs {tr['elite_cem']}"
+    got = nat.finish()
+    cx, cy, v_best, steer_best, mean_param, out = ref
+    close("cx", got["cx"], cx, rtol=1e-4, atol=1e-4)
+    close("cy", got["cy"], cy, rtol=1e-4, atol=1e-4)
+    close("v_best", got["v_best"], v_best, rtol=1e-4, atol=1e-4)
+    close("steering", got["steering"], steer_best, rtol=1e-4, atol=1e-5)
+    close("mean_param", got["mean_param"], mean_param, rtol=1e-4, atol=1e-4)
+    print(f"CARLA {cost} n={n} B={B} {town} tick {tick}: 20 iterations in lockstep; obs {float(got['cost_obs'])} "
+          f"lane {float(got['cost_lane'])}; explained beta-CEM partings {parted}")
+
+
+def test_carla_dropin_interface(native):
+    """The drop-in class with the reference's constructor and call signature
+    (carla/main_carla.py:186-194, 378-382) returns the reference's tuple."""
+    sys.path.insert(0, CARLA)
+    try:
+        for m in [m for m in list(sys.modules) if m == "optimizer" or m.startswith("optimizer.")]:
+            sys.modules.pop(m)
+        from optimizer import cem
+        prob = cem.CEM(4, 1, 3, 0.1, 60, "gaussian", "Town05", 0.0, 0.0)
+    finally:
+        sys.path.remove(CARLA)
+        for m in [m for m in list(sys.modules) if m == "optimizer" or m.startswith("optimizer.")]:
+            sys.modules.pop(m)
+    init, xo, yo, path = _tick(40, 3, 60)
+    for fn in (prob.compute_cem_mmd, prob.compute_cem_cvar):
+        cx, cy, v, steer, mean = fn(1, init, MEAN, COV, xo, yo, 10.0, path["x_path"], path["y_path"],
+                                    path["arc_vec"], path["Fx_dot"], path["Fy_dot"], path["kappa"])
+        assert cx.shape == (11,) and cy.shape == (11,) and v.shape == (100,) and steer.shape == (100,)
+        assert mean.shape == (8,) and np.all(np.isfinite(cx)) and np.all(np.isfinite(steer))
+        assert np.all(np.abs(steer) < np.pi / 2)
+    with pytest.raises(NotImplementedError):
+        prob.compute_cem_det()
