@@ -12,6 +12,7 @@ static mmd_opt free run (tests/test_gpu_free_run.py), a candidate whose
 beta-CEM parted from the oracle's is accepted only at the near-tie that
 explains it (tests/parity.py: beta_divergence), and must not move an elite set.
 """
+import importlib
 import importlib.util
 import os
 import sys
@@ -37,13 +38,25 @@ def _replay():
     return mod
 
 
+def carla_package():
+    """The CARLA drop-in package (mpc-mmd_amd/carla/optimizer).  It is named
+    ``optimizer`` like the static one (the reference has two packages of that
+    name), so the tests, which already import the static package, load it
+    under an alias."""
+    name = "mpcmmd_carla_optimizer"
+    if name not in sys.modules:
+        d = os.path.join(CARLA, "optimizer")
+        spec = importlib.util.spec_from_file_location(name, os.path.join(d, "__init__.py"),
+                                                      submodule_search_locations=[d])
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules[name] = mod
+        spec.loader.exec_module(mod)
+    return name
+
+
 def _tick(k, num_obs=3, H=60):
     R = _replay()
-    sys.path.insert(0, CARLA)
-    try:
-        from optimizer.cem_helper import Helper
-    finally:
-        sys.path.remove(CARLA)
+    Helper = importlib.import_module(carla_package() + ".cem_helper").Helper
     rec = R.record_synthetic(ticks=k + 1)
     return R.tick_inputs(rec, k, Helper(num_prime=H), num_obs)
 
@@ -134,16 +147,8 @@ def test_carla_tick_lockstep(native, cost, n, B, tick, town):
 def test_carla_dropin_interface(native):
     """The drop-in class with the reference's constructor and call signature
     (carla/main_carla.py:186-194, 378-382) returns the reference's tuple."""
-    sys.path.insert(0, CARLA)
-    try:
-        for m in [m for m in list(sys.modules) if m == "optimizer" or m.startswith("optimizer.")]:
-            sys.modules.pop(m)
-        from optimizer import cem
-        prob = cem.CEM(4, 1, 3, 0.1, 60, "gaussian", "Town05", 0.0, 0.0)
-    finally:
-        sys.path.remove(CARLA)
-        for m in [m for m in list(sys.modules) if m == "optimizer" or m.startswith("optimizer.")]:
-            sys.modules.pop(m)
+    cem = importlib.import_module(carla_package() + ".cem")
+    prob = cem.CEM(4, 1, 3, 0.1, 60, "gaussian", "Town05", 0.0, 0.0)
     init, xo, yo, path = _tick(40, 3, 60)
     for fn in (prob.compute_cem_mmd, prob.compute_cem_cvar):
         cx, cy, v, steer, mean = fn(1, init, MEAN, COV, xo, yo, 10.0, path["x_path"], path["y_path"],
