@@ -102,8 +102,12 @@ def test_carla_tick_lockstep(native, cost, n, B, tick, town):
         nat.iterate(t, 1)
         nat.sync()
         tr = trace[t]
-        close(f"steer[{t}]", nat.read("steer").reshape(-1, 100)[:B], tr["steer"], rtol=0, atol=0)
-        close(f"kappa[{t}]", nat.read("kappa_i").reshape(-1, 100)[:B], tr["kappa"], rtol=0, atol=0)
+        # bit-exact while the carries are (cvar; mmd_opt's first iteration).  From
+        # mmd_opt's second iteration on the population carries the beta-CEM's
+        # fp32 MMD costs (GPU vs oracle ~1e-7 relative) through the CEM weights
+        tol = (0.0, 0.0) if cost == "cvar" or t == 0 else (1e-4, 1e-6)
+        close(f"steer[{t}]", nat.read("steer").reshape(-1, 100)[:B], tr["steer"], rtol=tol[0], atol=tol[1])
+        close(f"kappa[{t}]", nat.read("kappa_i").reshape(-1, 100)[:B], tr["kappa"], rtol=tol[0], atol=tol[1])
         obs_g, lane_g, des_g = nat.read("obs_cost")[:B], nat.read("lane_cost")[:B], nat.read("lane_des")[:B]
         fl = 1e-2 if cost == "mmd_opt" else 1e-5
         ok = np.abs(obs_g - tr["obs"]) <= fl + 1e-4 * np.abs(tr["obs"])
