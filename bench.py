@@ -356,12 +356,97 @@ def run_workload(name, steps, warmup, profile_steps, rank, world, local, dist=No
                 kernels={k: v[1] / profile_steps for k, v in busy.items()})
 
 
+CARLA = os.path.join(PKG, "carla")
+# BASELINE configs[4]: the CARLA optimizer (carla/optimizer/cem.py), mmd_opt + cvar back to back per
+# simulator tick at H = 60, num_batch 100 (cem.py:138), num_obs 3 (README CARLA commands), replayed ticks
+CARLA_WORKLOAD = dict(desc="CARLA replay (synthetic Town05 recording), compute_cem_mmd + compute_cem_cvar back to "
+                           "back per tick, H=60, num_batch=100, num_obs=3, num_reduced_set=10 (mmd: 100 mother rows)",
+                      baseline="configs[4]", num_reduced=10, num_obs=3, num_prime=60, noise="gaussian", level=0.1,
+                      num_batch=100, town="Town05", budget_ms=50.0)
+
+
+def _carla_modules():
+    """The CARLA drop-in package (named ``optimizer`` like the static one) and
+    the replay module, loaded under aliases."""
+    import importlib
+    import importlib.util
+    name = "mpcmmd_carla_optimizer"
+    if name not in sys.modules:
+        d = os.path.join(CARLA, "optimizer")
+        spec = importlib.util.spec_from_file_location(name, os.path.join(d, "__init__.py"),
+                                                      submodule_search_locations=[d])
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules[name] = mod
+        spec.loader.exec_module(mod)
+    spec = importlib.util.spec_from_file_location("mpcmmd_carla_replay", os.path.join(CARLA, "replay.py"))
+    rep = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(rep)
+    return importlib.import_module(name + ".cem"), rep
+
+
+def run_carla(ticks, warmup, local, n=None):
+    """Per-tick time of the CARLA loop body on replayed ticks
+    (carla/main_carla.py:345-382): the path / obstacle preprocessing through
+    the drop-in's helpers, then compute_cem_mmd and compute_cem_cvar, each
+    carrying its own mean_param to the next tick (:378).  Wall-clock per
+    tick (synchronous calls, as the driver makes them), against the 50 ms
+    tick of carla_simulation.py:20."""
+    import torch
+    w = dict(CARLA_WORKLOAD)
+    if n is not None:
+        w["num_reduced"] = n
+    cem, rep = _carla_modules()
+    prob = cem.CEM(w["num_reduced"], 1, w["num_obs"], w["level"], w["num_prime"], w["noise"], w["town"], 0.0, 0.0,
+                   device=local)
+    stride = 5
+    rec = rep.record_synthetic(ticks=(warmup + ticks) * stride + 1, town=w["town"])
+    mean0 = np.array([10.0] * 4 + [0.0] * 4, np.float32)                  # main_carla.py:306-318
+    cov = np.diag([20.0] * 4 + [100.0] * 4).astype(np.float32)
+    means = {"mmd_opt": mean0.copy(), "cvar": mean0.copy()}
+    rows = []
+    for i in range(warmup + ticks):
+        k = i * stride
+        t0 = time.perf_counter()
+        init, xo, yo, path = rep.tick_inputs(rec, k, prob.cem_helper, w["num_obs"])
+        t1 = time.perf_counter()
+        args = (path["x_path"], path["y_path"], path["arc_vec"], path["Fx_dot"], path["Fy_dot"], path["kappa"])
+        r1 = prob.compute_cem_mmd(k, init, means["mmd_opt"], cov, xo, yo, 10.0, *args)
+        t2 = time.perf_counter()
+        r2 = prob.compute_cem_cvar(k, init, means["cvar"], cov, xo, yo, 10.0, *args)
+        t3 = time.perf_counter()
+        means["mmd_opt"], means["cvar"] = r1[4], r2[4]
+        if i >= warmup:
+            rows.append((t1 - t0, t2 - t1, t3 - t2, t3 - t0))
+    torch.cuda.synchronize()
+    a = np.array(rows) * 1e3
+    # one profiled tick: per-kernel HIP-event times of both solves
+    h = prob.handle
+    h.profile(True)
+    init, xo, yo, path = rep.tick_inputs(rec, 0, prob.cem_helper, w["num_obs"])
+    args = (path["x_path"], path["y_path"], path["arc_vec"], path["Fx_dot"], path["Fy_dot"], path["kappa"])
+    prob.compute_cem_mmd(0, init, mean0, cov, xo, yo, 10.0, *args)
+    prob.compute_cem_cvar(0, init, mean0, cov, xo, yo, 10.0, *args)
+    kt = {k: v for k, v in h.kernel_times().items() if v[0] > 0}
+    h.profile(False)
+    gpu_ms = sum(v[1] for v in kt.values())
+    return {"baseline": w["baseline"], "workload": w["desc"], "num_reduced_set": w["num_reduced"], "ticks": ticks,
+            "value": 1e3 / float(np.mean(a[:, 3])), "unit": "ticks/s",
+            "ms_per_tick": float(np.mean(a[:, 3])), "median_ms_per_tick": float(np.median(a[:, 3])),
+            "p90_ms_per_tick": float(np.percentile(a[:, 3], 90)), "budget_ms": w["budget_ms"],
+            "ticks_within_budget": float(np.mean(a[:, 3] <= w["budget_ms"])),
+            "ms_preprocess": float(np.mean(a[:, 0])), "ms_mmd": float(np.mean(a[:, 1])),
+            "ms_cvar": float(np.mean(a[:, 2])),
+            "profiled_tick_gpu_ms": gpu_ms,
+            "kernels_ms_per_tick": {k: v[1] for k, v in kt.items()},
+            "launches_per_tick": int(sum(v[0] for v in kt.values()))}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="mmd_opt", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="mmd_opt", choices=sorted(WORKLOADS) + ["carla"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--profile-steps", type=int, default=20)
     ap.add_argument("--extra", type=int, default=1, help="N = 1: also time the other BASELINE workloads (0 = skip)")
@@ -376,6 +461,10 @@ def main():
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world} (launch N>1 with torchrun)")
     torch.cuda.set_device(local)
+    if a.workload == "carla":  # configs[4] alone (one GPU, a real-time tick loop: no sharding)
+        print(json.dumps({"metric": "CARLA ticks/s (mmd_opt + cvar per tick)", **run_carla(a.steps, a.warmup, local)}),
+              flush=True)
+        return
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     r = run_workload(a.workload, a.steps, a.warmup, a.profile_steps, rank, world, local, dist if world > 1 else None)
@@ -429,6 +518,8 @@ def main():
                                "median_ms_per_step": float(np.median(x["step_ms"])),
                                "solves_per_s": steps / x["elapsed"] / T, "roofline": x["roof"],
                                "kernels_ms_per_step": x["kernels"]}
+            for nn in (10, 22):  # configs[4]: num_reduced_set 10 (the line's workload) and 22 (configs[1]'s n)
+                extra["carla" if nn == 10 else f"carla_n{nn}"] = run_carla(ticks=10, warmup=2, local=local, n=nn)
             line["extra_workloads"] = extra
         print(json.dumps(line), flush=True)
     if world > 1:
