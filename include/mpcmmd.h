@@ -228,6 +228,14 @@ int mpcmmd_path_parameters(int32_t num_path, const float* x_path, const float* y
 int mpcmmd_global_to_frenet(const mpcmmd_path* path, int32_t count, const float* x, const float* y, const float* v,
                             const float* vdot, const float* psi, const float* psidot, float* out);
 
+/* Whole-solve HIP graphs: with enable != 0, mpcmmd_iterate(h, 0, T) captures
+ * the solve's launch sequence once per (cost, path length, external draws,
+ * configurations) and replays it with one hipGraphLaunch (handles whose
+ * launches use one stream, i.e. fewer than 1024 candidates).  Results are
+ * identical to the launched sequence.  Default off (environment MPCMMD_GRAPH=1
+ * turns it on at create). */
+int mpcmmd_set_graphs(mpcmmd_handle* h, int32_t enable);
+
 /* Per-kernel HIP-event timing (on the handle's stream).  When enabled, every
  * launch of every kernel is bracketed by events; mpcmmd_kernel_times returns,
  * per kernel id, the number of launches and the total milliseconds since the

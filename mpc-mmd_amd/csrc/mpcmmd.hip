@@ -113,6 +113,11 @@ struct mpcmmd_handle {
   bool groups_forced = false;
   hipStream_t gstream[kMaxGroups] = {};
   hipEvent_t gev_start = nullptr, gev_done[kMaxGroups] = {};
+  // whole-solve graphs: mpcmmd_iterate(0, T) captured once per (cost, path
+  // length, external draws, configurations) and replayed (one hipGraphLaunch
+  // instead of ~150 launches per outer iteration)
+  bool graphs = false;
+  std::map<std::tuple<int, int, int, int>, std::pair<hipGraph_t, hipGraphExec_t>> gexec;
   // profiling
   bool prof = false;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -642,6 +647,7 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     // kernel sums (B = 1024: 82.2 -> 92.8 steps/s; four groups: 72.6)
     if (BT >= 1024) h->groups = 2;
     h->groups_forced = std::getenv("MPCMMD_GROUPS") != nullptr;
+    if (const char* g = std::getenv("MPCMMD_GRAPH")) h->graphs = std::atoi(g) != 0;
     if (const char* g = std::getenv("MPCMMD_GROUPS")) h->groups = std::max(1, std::min(mpcmmd_handle::kMaxGroups, std::atoi(g)));
     if (h->groups > 1) {
       HIPC(hipEventCreateWithFlags(&h->gev_start, hipEventDisableTiming));
@@ -676,6 +682,10 @@ void mpcmmd_destroy(mpcmmd_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (auto& kv : h->gexec) {
+    (void)hipGraphExecDestroy(kv.second.second);
+    (void)hipGraphDestroy(kv.second.first);
+  }
   for (int g = 0; g < mpcmmd_handle::kMaxGroups; ++g)  // group streams drained before their buffers go
     if (h->gstream[g]) (void)hipStreamSynchronize(h->gstream[g]);
   for (auto& kv : h->bufs) (void)hipFree(kv.second.first);
@@ -962,16 +972,53 @@ int mpcmmd_iterate(mpcmmd_handle* h, int32_t t_begin, int32_t count) {
   if (t_begin < 0 || count < 0 || t_begin + count > h->T) return fail(MPCMMD_E_INVALID, "iteration range");
   return guarded([&] {
     check_device(h);
-    for (int t = t_begin; t < t_begin + count; ++t) {
-      if (!h->ext_roll || !h->ext_res) {
-        if (h->ext_roll != h->ext_res) throw std::invalid_argument("roll and resample draws go together");
-        run_stage(h, 0, t);
+    auto body = [&] {
+      for (int t = t_begin; t < t_begin + count; ++t) {
+        if (!h->ext_roll || !h->ext_res) {
+          if (h->ext_roll != h->ext_res) throw std::invalid_argument("roll and resample draws go together");
+          run_stage(h, 0, t);
+        }
+        run_stage(h, 1, t);
+        run_stage(h, 2, t);
+        run_stage(h, 3, t);
       }
-      run_stage(h, 1, t);
-      run_stage(h, 2, t);
-      run_stage(h, 3, t);
-      h->last_t = t;
+    };
+    // a whole solve on one stream (the candidate groups of large batches
+    // fork onto other streams: launched directly)
+    const bool one_stream = h->p.Bt < 1024 && !h->groups_forced;
+    if (h->graphs && !h->prof && one_stream && t_begin == 0 && count == h->T) {
+      if (h->cost == MPCMMD_COST_MMD_OPT) ensure_sel0(h);  // host read-back: never inside a capture
+      const auto key = std::make_tuple(h->cost, h->p.P, int(h->ext_roll), h->G);
+      auto it = h->gexec.find(key);
+      if (it == h->gexec.end()) {
+        hipGraph_t g = nullptr;
+        HIPC(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+        try {
+          body();
+        } catch (...) {
+          (void)hipStreamEndCapture(h->stream, &g);
+          if (g) (void)hipGraphDestroy(g);
+          throw;
+        }
+        HIPC(hipStreamEndCapture(h->stream, &g));
+        hipGraphExec_t e = nullptr;
+        HIPC(hipGraphInstantiate(&e, g, nullptr, nullptr, 0));
+        it = h->gexec.emplace(key, std::make_pair(g, e)).first;
+      }
+      HIPC(hipGraphLaunch(it->second.second, h->stream));
+    } else {
+      body();
     }
+    h->last_t = t_begin + count - 1;
+    return MPCMMD_OK;
+  });
+}
+
+int mpcmmd_set_graphs(mpcmmd_handle* h, int32_t enable) {
+  if (!h) return fail(MPCMMD_E_INVALID, "null handle");
+  return guarded([&] {
+    check_device(h);
+    h->graphs = enable != 0;
     return MPCMMD_OK;
   });
 }

@@ -28,7 +28,7 @@ SYMBOLS = (
     "mpcmmd_host_constant", "mpcmmd_obs_dynamic_traj", "mpcmmd_validate", "mpcmmd_create_batch",
     "mpcmmd_max_configs", "mpcmmd_solve_batch", "mpcmmd_begin_batch", "mpcmmd_finish_batch",
     "mpcmmd_carla_begin", "mpcmmd_carla_solve", "mpcmmd_path_smoothing", "mpcmmd_path_parameters",
-    "mpcmmd_global_to_frenet",
+    "mpcmmd_global_to_frenet", "mpcmmd_set_graphs",
 )
 
 
@@ -127,6 +127,7 @@ def lib():
     L.mpcmmd_validate.argtypes = [C.POINTER(ValidateArgs)]
     L.mpcmmd_obs_dynamic_traj.argtypes = [C.c_int32, fp, fp, fp, fp, fp, C.c_float, fp, fp]
     cargs = [vp, C.c_int32, C.c_int32, fp, fp, fp, fp, fp, C.c_float, C.POINTER(Path), C.POINTER(Draws)]
+    L.mpcmmd_set_graphs.argtypes = [vp, C.c_int32]
     L.mpcmmd_carla_begin.argtypes = cargs
     L.mpcmmd_carla_solve.argtypes = cargs + [C.POINTER(Result)]
     L.mpcmmd_path_smoothing.argtypes = [C.c_int32, fp, fp, C.c_float, fp, fp]
@@ -420,6 +421,10 @@ class Handle:
     # -- streams / profiling -----------------------------------------------------
     def set_stream(self, stream_ptr):
         check(self._L.mpcmmd_set_stream(self._h, C.c_void_p(stream_ptr)))
+
+    def set_graphs(self, enable):
+        """mpcmmd_set_graphs: replay whole solves as captured HIP graphs."""
+        check(self._L.mpcmmd_set_graphs(self._h, 1 if enable else 0))
 
     def profile(self, enable):
         check(self._L.mpcmmd_profile(self._h, 1 if enable else 0))
