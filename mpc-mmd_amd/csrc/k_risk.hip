@@ -14,6 +14,8 @@
 // (O obstacles, staged in LDS) and the lane bars into running maxima, so
 // the stage reads only the candidate's H controls and the shared noise rows
 // (L2-resident, [H][S] for coalescing) and writes two floats per candidate.
+#include <cstdlib>
+
 #include "block.hpp"
 #include "kernels.hpp"
 #include "rng.hpp"
@@ -242,6 +244,67 @@ __global__ __launch_bounds__(256) void k_beta_planes(Params p, int t) {
   }
 }
 
+// The same draws with one lane per CANDIDATE (64 candidates of one
+// configuration) and a wave walking 16 rows of one step: the attempt-table
+// entry of a (row, step) is then one value for the whole wave (scalar loads),
+// so the alpha-independent squeeze decision -- which decides whether the fp32 /
+// fp64 log test and the later attempts run at all -- is wave-uniform, and a
+// wave executes those rare paths only where its (row, step) needs them
+// instead of whenever any of its 64 rows does (row lanes: nearly always).
+// Per lane the alpha-dependent transforms and the combine are the identical
+// functions of k_beta_planes (bit-identical draws).  The [64 rows][64
+// candidates] tile goes through LDS so the planes are stored as 256-byte row
+// runs per candidate.
+constexpr int kBpRows = 64;
+
+__global__ __launch_bounds__(256) void k_beta_planes_c(Params p, int t) {
+  const int S = p.S, H = p.H;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r0 = blockIdx.x * kBpRows, h = blockIdx.y;
+  const int groups = (p.B + 63) / 64;
+  const int g = blockIdx.z / groups, j0 = (blockIdx.z - g * groups) * 64;
+  const int nc = min(64, p.B - j0);
+  const double* gt = p.gtab + size_t(g) * gtab_stride(S, H);
+  const size_t plane = size_t(S) * H, sl = size_t(kGammaTabAttempts) * 4 * plane;
+  __shared__ float tile[2][kBpRows][65];
+  const int c = min(lane, nc - 1);
+  const uint32_t b = uint32_t(g) * p.B + j0 + c;
+  const float fa = fabsf(p.acc[size_t(b) * 100 + h]), fs = fabsf(p.steer[size_t(b) * 100 + h]);
+  const MtConst m[4] = {mt_const(double(2.0f * fa)), mt_const(double(5.0f * fa)), mt_const(double(2.0f * fs)),
+                        mt_const(double(5.0f * fs))};
+  for (int i = 0; i < kBpRows / 4; ++i) {
+    const int rl = w * (kBpRows / 4) + i, r = r0 + rl;
+    if (r >= S) break;
+    const size_t at = size_t(h) * S + r;
+    auto draw = [&](int k, float f, float& out) {
+      double ga, ua, gb, ub;
+      const double* ta = gt + k * sl + at;
+      const double* tb = gt + (k + 1) * sl + at;
+      const bool ok = (tab_try(m[k], TabAtt{ta[0], ta[2 * plane], ta[3 * plane]}, ga, ua) ||
+                       gamma_tab_from(m[k], gt + k * sl, plane, at, 1, ga, ua)) &&
+                      (tab_try(m[k + 1], TabAtt{tb[0], tb[2 * plane], tb[3 * plane]}, gb, ub) ||
+                       gamma_tab_from(m[k + 1], gt + (k + 1) * sl, plane, at, 1, gb, ub));
+      if (ok) out = beta_combine(double(2.0f * f), double(5.0f * f), 2.0, 5.0, ga, ua, gb, ub);
+      return ok;
+    };
+    float nba = 0.0f, nbs = 0.0f;
+    if (draw(0, fa, nba) && draw(2, fs, nbs)) {
+      tile[0][rl][lane] = nba;
+      tile[1][rl][lane] = nbs;
+    } else if (lane < nc) {  // more attempts than tabulated: k_beta_fix (after this launch) writes it
+      const unsigned slot = atomicAdd(p.bfix_n, 1u);
+      p.bfix[slot] = (b * uint32_t(H) + uint32_t(h)) * uint32_t(S) + uint32_t(r);
+    }
+  }
+  __syncthreads();
+  const int nr = min(kBpRows, S - r0);
+  for (int q = threadIdx.x; q < nc * 2 * kBpRows; q += blockDim.x) {
+    const int rl = q & (kBpRows - 1), kc = q / kBpRows, k = kc & 1, cl = kc >> 1;
+    if (rl >= nr) continue;
+    p.bplane[(size_t(g) * p.B + j0 + cl) * 2 * H * S + (size_t(k) * H + h) * S + r0 + rl] = tile[k][rl][cl];
+  }
+}
+
 // the deferred elements of k_beta_planes, through the full sampler
 __global__ __launch_bounds__(256) void k_beta_fix(Params p, int t) {
   const int S = p.S, H = p.H;
@@ -261,8 +324,19 @@ __global__ __launch_bounds__(256) void k_beta_fix(Params p, int t) {
 }  // namespace
 
 void launch_beta_planes(const Params& p, int t, hipStream_t s) {
-  const int groups = (p.B + kBetaCands - 1) / kBetaCands;
-  hipLaunchKernelGGL(k_beta_planes, dim3((p.S + kBetaRows - 1) / kBetaRows, p.H, p.G * groups), dim3(256), 0, s, p, t);
+  static const bool rows = [] {  // MPCMMD_BETA_ROWS=1: the row-lane kernel (A/B)
+    const char* e = std::getenv("MPCMMD_BETA_ROWS");
+    return e && std::atoi(e) != 0;
+  }();
+  if (rows) {
+    const int groups = (p.B + kBetaCands - 1) / kBetaCands;
+    hipLaunchKernelGGL(k_beta_planes, dim3((p.S + kBetaRows - 1) / kBetaRows, p.H, p.G * groups), dim3(256), 0, s, p,
+                       t);
+  } else {
+    const int groups = (p.B + 63) / 64;
+    hipLaunchKernelGGL(k_beta_planes_c, dim3((p.S + kBpRows - 1) / kBpRows, p.H, p.G * groups), dim3(256), 0, s, p,
+                       t);
+  }
   hipLaunchKernelGGL(k_beta_fix, dim3(256), dim3(256), 0, s, p, t);
 }
 
