@@ -257,47 +257,114 @@ __global__ __launch_bounds__(256) void k_beta_planes(Params p, int t) {
 // runs per candidate.
 constexpr int kBpRows = 64;
 
+// Per lane (candidate) and gamma stream: the Marsaglia-Tsang constants in
+// fp64 (the exact decisions, fallbacks) and the fp32 forms of the common path.
+struct MtLane {
+  MtConst m;
+  float c, log2d;
+};
+DEVI MtLane mt_lane(double alpha) {
+  const MtConst m = mt_const(alpha);
+  return MtLane{m, float(m.c), __builtin_amdgcn_logf(float(m.d))};
+}
+
+// Attempt 0 of one gamma from the staged table entry (x, log u, +-log w):
+// the fp32 common path.  v = 1 + c x in fp32 decides v > 0 unless it is
+// within 1e-5 of 0 (then fp64, the exact test); the squeeze decision is the
+// stored sign of log w (wave-uniform); the log test is mt_log_test's fp32
+// test with its fp64 re-check.  Returns log2 G' = log2 d + 3 log2 v (fp32)
+// and the boost log-uniform; false = rejected (attempts 1.. follow).
+DEVI bool tab0_fast(const MtLane& L, double x, double lu, double lw, float& lg, double& lub) {
+  const float xf = float(x);
+  const float vf = 1.0f + L.c * xf;
+  float v = vf;
+  if (!(fabsf(vf) > 1e-5f)) {
+    const double vd = 1.0 + L.m.c * x;
+    if (!(vd > 0.0)) return false;
+    v = float(vd);
+  } else if (!(vf > 0.0f)) {
+    return false;
+  }
+  if (!(lw < 0.0)) {  // the squeeze rejected: the log test on v^3
+    const double vd = 1.0 + L.m.c * x;
+    if (!mt_log_test(x, lu, L.m.d, vd * vd * vd)) return false;
+  }
+  lg = L.log2d + 3.0f * __builtin_amdgcn_logf(v);
+  lub = -fabs(lw);
+  return true;
+}
+
+// Beta(a, b) = 1 / (1 + 2^(log2 Gb - log2 Ga)) from the gammas' log2 G' and
+// boost log-uniforms (beta_combine's formula, the log2 G' given).
+DEVI float beta_from_logs(double a, double b, double ra, double rb, float lga, double ua, float lgb, double ub) {
+  if (a == 0.0 && b == 0.0) return (ua * rb > ub * ra) ? 1.0f : 0.0f;
+  const bool ka = a < 1.0, kb = b < 1.0;
+  float e = 0.0f;
+  if (ka || kb) {
+    const double fa = ka ? a : 1.0, fb = kb ? b : 1.0;
+    e = float(((kb ? ub : 0.0) * fa - (ka ? ua : 0.0) * fb) * __builtin_amdgcn_rcp(fa * fb));
+  }
+  const float d = (lgb - lga) + 1.44269504088896340736f * e;
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(d));
+}
+
+// The same draws with one lane per CANDIDATE (64 candidates of one
+// configuration) and a wave walking 16 rows of one step: the attempt-table
+// entry of a (row, step) is one value for the whole wave, so the
+// alpha-independent squeeze decision -- which decides whether the log test
+// runs at all -- is wave-uniform.  The workgroup's 64 rows of attempt 0 are
+// staged in LDS (one coalesced pass); attempt 0 runs the fp32 common path
+// (tab0_fast), rejected attempts the fp64 table path of k_beta_planes,
+// longer chains go to k_beta_fix.  The [64 rows][64 candidates] result tile
+// goes through LDS so the planes are stored as 256-byte row runs.
 __global__ __launch_bounds__(256) void k_beta_planes_c(Params p, int t) {
   const int S = p.S, H = p.H;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r0 = blockIdx.x * kBpRows, h = blockIdx.y;
   const int groups = (p.B + 63) / 64;
   const int g = blockIdx.z / groups, j0 = (blockIdx.z - g * groups) * 64;
-  const int nc = min(64, p.B - j0);
+  const int nc = min(64, p.B - j0), nr = min(kBpRows, S - r0);
   const double* gt = p.gtab + size_t(g) * gtab_stride(S, H);
   const size_t plane = size_t(S) * H, sl = size_t(kGammaTabAttempts) * 4 * plane;
+  __shared__ double t0x[4][kBpRows], t0u[4][kBpRows], t0w[4][kBpRows];
   __shared__ float tile[2][kBpRows][65];
+  for (int q = threadIdx.x; q < 4 * kBpRows; q += blockDim.x) {  // attempt 0, streams acc A/B, steer A/B
+    const int k = q / kBpRows, rl = q - k * kBpRows;
+    const double* e = gt + k * sl + size_t(h) * S + r0 + min(rl, nr - 1);
+    t0x[k][rl] = e[0];
+    t0u[k][rl] = e[2 * plane];
+    t0w[k][rl] = e[3 * plane];
+  }
   const int c = min(lane, nc - 1);
   const uint32_t b = uint32_t(g) * p.B + j0 + c;
   const float fa = fabsf(p.acc[size_t(b) * 100 + h]), fs = fabsf(p.steer[size_t(b) * 100 + h]);
-  const MtConst m[4] = {mt_const(double(2.0f * fa)), mt_const(double(5.0f * fa)), mt_const(double(2.0f * fs)),
-                        mt_const(double(5.0f * fs))};
+  const double aa = double(2.0f * fa), ab = double(5.0f * fa), sa = double(2.0f * fs), sb = double(5.0f * fs);
+  const MtLane L[4] = {mt_lane(aa), mt_lane(ab), mt_lane(sa), mt_lane(sb)};
+  __syncthreads();
   for (int i = 0; i < kBpRows / 4; ++i) {
     const int rl = w * (kBpRows / 4) + i, r = r0 + rl;
-    if (r >= S) break;
+    if (rl >= nr) break;
     const size_t at = size_t(h) * S + r;
-    auto draw = [&](int k, float f, float& out) {
-      double ga, ua, gb, ub;
-      const double* ta = gt + k * sl + at;
-      const double* tb = gt + (k + 1) * sl + at;
-      const bool ok = (tab_try(m[k], TabAtt{ta[0], ta[2 * plane], ta[3 * plane]}, ga, ua) ||
-                       gamma_tab_from(m[k], gt + k * sl, plane, at, 1, ga, ua)) &&
-                      (tab_try(m[k + 1], TabAtt{tb[0], tb[2 * plane], tb[3 * plane]}, gb, ub) ||
-                       gamma_tab_from(m[k + 1], gt + (k + 1) * sl, plane, at, 1, gb, ub));
-      if (ok) out = beta_combine(double(2.0f * f), double(5.0f * f), 2.0, 5.0, ga, ua, gb, ub);
-      return ok;
+    // one gamma: the fp32 attempt 0, else the fp64 table attempts 1..3
+    auto gam = [&](int k, float& lg, double& lub) {
+      if (tab0_fast(L[k], t0x[k][rl], t0u[k][rl], t0w[k][rl], lg, lub)) return true;
+      double gg;
+      if (!gamma_tab_from(L[k].m, gt + k * sl, plane, at, 1, gg, lub)) return false;
+      lg = __builtin_amdgcn_logf(float(gg));
+      return true;
     };
-    float nba = 0.0f, nbs = 0.0f;
-    if (draw(0, fa, nba) && draw(2, fs, nbs)) {
-      tile[0][rl][lane] = nba;
-      tile[1][rl][lane] = nbs;
+    float lg0, lg1, lg2, lg3;
+    double u0, u1, u2, u3;
+    const bool ok = gam(0, lg0, u0) && gam(1, lg1, u1) && gam(2, lg2, u2) && gam(3, lg3, u3);
+    if (ok) {
+      tile[0][rl][lane] = beta_from_logs(aa, ab, 2.0, 5.0, lg0, u0, lg1, u1);
+      tile[1][rl][lane] = beta_from_logs(sa, sb, 2.0, 5.0, lg2, u2, lg3, u3);
     } else if (lane < nc) {  // more attempts than tabulated: k_beta_fix (after this launch) writes it
       const unsigned slot = atomicAdd(p.bfix_n, 1u);
       p.bfix[slot] = (b * uint32_t(H) + uint32_t(h)) * uint32_t(S) + uint32_t(r);
     }
   }
   __syncthreads();
-  const int nr = min(kBpRows, S - r0);
   for (int q = threadIdx.x; q < nc * 2 * kBpRows; q += blockDim.x) {
     const int rl = q & (kBpRows - 1), kc = q / kBpRows, k = kc & 1, cl = kc >> 1;
     if (rl >= nr) continue;
