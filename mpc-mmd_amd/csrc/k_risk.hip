@@ -372,6 +372,209 @@ __global__ __launch_bounds__(256) void k_beta_planes_c(Params p, int t) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused baseline risk with one lane per CANDIDATE (cvar / saa / mmd_random;
+// both noise models).  A wave runs one noise row r for 64 candidates of one
+// configuration, so everything indexed by (row, step) -- the Gaussian normals
+// and, for Beta noise, the attempt-table entries of the four gamma streams
+// (cem_helper.py:405-443: one realisation shared by every candidate, Q2) --
+// is one value per wave, and the Beta draws are made inside the rollout: no
+// [B][2][H][S] planes are written or read.  The alpha-independent squeeze
+// decision being wave-uniform, the log test and the later attempts run only
+// where their (row, step) needs them.  The per-(candidate, step) gamma
+// constants come from k_mt_tab.  Rollout, collision residual and lane bars
+// are k_risk_baseline's arithmetic; the per-row maxima go to Params::rbar and
+// k_risk_reduce applies the reducer (one workgroup per candidate).
+struct MtTab {
+  float4 c;      // c = 1 / sqrt(9 d) of the four gammas (acc a, acc b, steer a, steer b); NaN: control 0
+  float4 l2d;    // log2 d
+  double4 rinv;  // 1 / alpha where alpha < 1 (the boost), else 0: acc a, acc b, steer a, steer b
+};
+
+__global__ __launch_bounds__(256) void k_mt_tab(Params p) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (h, b): b fastest
+  if (i >= p.Bt * p.H) return;
+  const int h = i / p.Bt, b = i - h * p.Bt;
+  const float fa = fabsf(p.acc[size_t(b) * 100 + h]), fs = fabsf(p.steer[size_t(b) * 100 + h]);
+  const double al[4] = {double(2.0f * fa), double(5.0f * fa), double(2.0f * fs), double(5.0f * fs)};
+  float c[4], l[4];
+  double r[4];
+  for (int k = 0; k < 4; ++k) {
+    const MtConst m = mt_const(al[k]);
+    c[k] = (k < 2 ? fa : fs) == 0.0f ? __int_as_float(0x7fc00000) : float(m.c);
+    l[k] = __builtin_amdgcn_logf(float(m.d));
+    r[k] = al[k] < 1.0 ? 1.0 / al[k] : 0.0;
+  }
+  MtTab* o = reinterpret_cast<MtTab*>(p.mttab) + i;
+  o->c = make_float4(c[0], c[1], c[2], c[3]);
+  o->l2d = make_float4(l[0], l[1], l[2], l[3]);
+  o->rinv = double4{r[0], r[1], r[2], r[3]};
+}
+
+// One gamma of a Beta draw: attempt 0 in fp32 (tab0_fast's decisions), else
+// the fp64 table / Philox path of gamma_parts_tab from attempt 0 (the same
+// decisions again, then the later attempts).  Returns log2 G' and log U_boost.
+DEVI void gamma_fused(float c, float l2d, double alpha, double x, double lu, double lw, const double* tab, int S,
+                      int H, int r, int h, uint32_t k0, uint32_t k1, uint32_t stream, float& lg, double& lub) {
+  const float vf = 1.0f + c * float(x);
+  bool ok;
+  float v = vf;
+  if (fabsf(vf) > 1e-5f) {
+    ok = vf > 0.0f;
+  } else {
+    const double vd = 1.0 + mt_const(alpha).c * x;
+    ok = vd > 0.0;
+    v = float(vd);
+  }
+  if (ok && !(lw < 0.0)) {  // the squeeze rejected: the exact log test
+    const MtConst m = mt_const(alpha);
+    const double vd = 1.0 + m.c * x;
+    ok = mt_log_test(x, lu, m.d, vd * vd * vd);
+  }
+  if (ok) {
+    lg = l2d + 3.0f * __builtin_amdgcn_logf(v);
+    lub = -fabs(lw);
+    return;
+  }
+  double g;
+  gamma_parts_tab(mt_const(alpha), tab, S, H, r, h, k0, k1, stream, uint32_t(r) * uint32_t(H) + uint32_t(h), g, lub);
+  lg = __builtin_amdgcn_logf(float(g));
+}
+
+DEVI float beta_fused(float fabs_ctl, double ra, double rb, float lga, double ua, float lgb, double ub) {
+  if (fabs_ctl == 0.0f) return (ua * 5.0 > ub * 2.0) ? 1.0f : 0.0f;  // Beta(0, 0): the alpha -> 0+ limit
+  const float e = (ra != 0.0 || rb != 0.0) ? float(ub * rb - ua * ra) : 0.0f;
+  const float d = (lgb - lga) + 1.44269504088896340736f * e;
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(d));
+}
+
+constexpr int kRcWaves = 4;
+
+__global__ __launch_bounds__(64 * kRcWaves) void k_roll_cand(Params p, int t) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int S = p.S, H = p.H, O = p.O;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int groups = (p.B + 63) / 64;
+  const int g = blockIdx.y / groups, j0 = (blockIdx.y - g * groups) * 64;
+  const int nc = min(64, p.B - j0);
+  const Cfg cf = cfg_of(p, g);
+  float* xo = reinterpret_cast<float*>(smem);
+  float* yo = xo + O * H;
+  float* ca = yo + O * H;  // [H][64] controls of the block's candidates
+  float* cs = ca + 64 * H;
+  for (int i = threadIdx.x; i < O * H; i += blockDim.x) {
+    xo[i] = cf.obs[i];
+    yo[i] = cf.obs[O * H + i];
+  }
+  for (int i = threadIdx.x; i < 64 * H; i += blockDim.x) {
+    const int h = i >> 6, cl = min(i & 63, nc - 1);
+    const size_t bb = size_t(g) * p.B + j0 + cl;
+    ca[i] = p.acc[bb * 100 + h];
+    cs[i] = p.steer[bb * 100 + h];
+  }
+  __syncthreads();
+  const int r = blockIdx.x * kRcWaves + w;
+  if (r >= S) return;
+  const int c = min(lane, nc - 1);
+  const size_t b = size_t(g) * p.B + j0 + c;
+  const size_t HS = size_t(H) * S;
+  const float* rl = cf.roll + size_t(t) * 3 * HS + r;  // [3][H][S]: uniform per wave
+  const bool beta = p.noise == 1;
+  const double* gt = beta ? cf.gtab : nullptr;
+  const size_t plane = HS, sl = size_t(kGammaTabAttempts) * 4 * plane;
+  const uint32_t k0 = iteration_key0(cf.idx_mpc, t), k1 = p.seed;
+  const MtTab* mt = reinterpret_cast<const MtTab*>(p.mttab);
+  float x = cf.st0[0], y = cf.st0[1], vx = cf.st0[2], vy = cf.st0[3], psi = cf.st0[4];
+  float cb = 0.0f, lb = 0.0f, ub = 0.0f;
+  bool nan = false;
+  for (int h = 0; h < H; ++h) {
+    for (int o = 0; o < O; ++o) {  // k_risk_baseline's residual (skip where f_bar <= 0 is certain)
+      const float xov = xo[o * H + h];
+      if (!(fabsf(x - xov) >= kObsA)) {
+        const float cc = f_bar(x, y, xov, yo[o * H + h]);
+        nan |= (cc != cc);
+        cb = fmaxf(cb, cc);
+      }
+    }
+    const float l1 = -y + p.y_lb, u1 = y - p.y_ub;
+    nan |= (y != y) | (x != x);
+    lb = fmaxf(lb, l1);
+    ub = fmaxf(ub, u1);
+    if (h == H - 1) break;
+    const float a = ca[h * 64 + lane], st = cs[h * 64 + lane];
+    const float nc2 = rl[2 * HS + size_t(h) * S];
+    float n0, n1;
+    if (!beta) {
+      n0 = rl[size_t(h) * S];
+      n1 = rl[HS + size_t(h) * S];
+    } else {
+      const MtTab m = mt[size_t(h) * p.Bt + b];
+      const size_t at = size_t(h) * S + r;
+      const double* e0 = gt + at;
+      const double* e1 = gt + sl + at;
+      const double* e2 = gt + 2 * sl + at;
+      const double* e3 = gt + 3 * sl + at;
+      const float fa = fabsf(a), fs = fabsf(st);
+      float lg0, lg1, lg2, lg3;
+      double u0, u1, u2, u3;
+      gamma_fused(m.c.x, m.l2d.x, double(2.0f * fa), e0[0], e0[2 * plane], e0[3 * plane], gt, S, H, r, h, k0, k1,
+                  kStreamGammaAccA, lg0, u0);
+      gamma_fused(m.c.y, m.l2d.y, double(5.0f * fa), e1[0], e1[2 * plane], e1[3 * plane], gt + sl, S, H, r, h, k0,
+                  k1, kStreamGammaAccB, lg1, u1);
+      gamma_fused(m.c.z, m.l2d.z, double(2.0f * fs), e2[0], e2[2 * plane], e2[3 * plane], gt + 2 * sl, S, H, r, h, k0,
+                  k1, kStreamGammaSteerA, lg2, u2);
+      gamma_fused(m.c.w, m.l2d.w, double(5.0f * fs), e3[0], e3[2 * plane], e3[3 * plane], gt + 3 * sl, S, H, r, h, k0,
+                  k1, kStreamGammaSteerB, lg3, u3);
+      n0 = beta_fused(fa, m.rinv.x, m.rinv.y, lg0, u0, lg1, u1);
+      n1 = beta_fused(fs, m.rinv.z, m.rinv.w, lg2, u2, lg3, u3);
+    }
+    float an, sn;
+    noisy_from(p, a, st, n0, n1, nc2, an, sn);
+    bicycle_step(x, y, vx, vy, psi, an, sn);
+  }
+  if (lane < nc) {
+    const float qnan = __int_as_float(0x7fc00000);
+    const size_t bs = size_t(p.Bt) * S;
+    p.rbar[b * S + r] = nan ? qnan : cb;
+    p.rbar[bs + b * S + r] = nan ? qnan : lb;
+    p.rbar[2 * bs + b * S + r] = nan ? qnan : ub;
+  }
+}
+
+// the reducers of k_risk_baseline over the per-row maxima of k_roll_cand
+__global__ __launch_bounds__(512) void k_risk_reduce(Params p, int t) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int S = p.S, b = blockIdx.x;
+  RiskLds L = carve(smem, p.O, p.H, S);
+  const size_t bs = size_t(p.Bt) * S;
+  for (int r = threadIdx.x; r < S; r += blockDim.x) {
+    L.cbar[r] = p.rbar[size_t(b) * S + r];
+    L.lb[r] = p.rbar[bs + size_t(b) * S + r];
+    L.ub[r] = p.rbar[2 * bs + size_t(b) * S + r];
+  }
+  __syncthreads();
+  ReduceScratch& rs = *L.rs;
+  float obs = 0.0f, lane = 0.0f;
+  if (p.cost == 2) {
+    obs = block_cvar(L.cbar, S, L.list, rs);
+    const float cl = block_cvar(L.lb, S, L.list, rs);
+    const float cu = block_cvar(L.ub, S, L.list, rs);
+    lane = cl + cu;
+  } else if (p.cost == 3) {
+    obs = float(block_count_pos(L.cbar, S, rs)) / float(S);
+    const int cl = block_count_pos(L.lb, S, rs);
+    const int cu = block_count_pos(L.ub, S, rs);
+    lane = float(cl + cu) / float(S);
+  } else {
+    obs = block_mmd(L.cbar, nullptr, S, 0.01f, 1000.0f, rs);
+    lane = 0.0f;
+  }
+  if (threadIdx.x == 0) {
+    p.obs_cost[b] = obs;
+    p.lane_cost[b] = lane;
+  }
+}
+
 // the deferred elements of k_beta_planes, through the full sampler
 __global__ __launch_bounds__(256) void k_beta_fix(Params p, int t) {
   const int S = p.S, H = p.H;
@@ -410,6 +613,25 @@ void launch_beta_planes(const Params& p, int t, hipStream_t s) {
 void launch_gamma_tab(const Params& p, int t, hipStream_t s) {
   const int total = kGammaTabStreams * kGammaTabAttempts * p.S * p.H;
   hipLaunchKernelGGL(k_gamma_tab, dim3((total + 255) / 256, p.G), dim3(256), 0, s, p, t);
+}
+
+bool risk_fused() {  // MPCMMD_RISK_FUSED=0: the row-lane rollouts over the Beta planes (A/B)
+  static const bool f = [] {
+    const char* e = std::getenv("MPCMMD_RISK_FUSED");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return f;
+}
+
+void launch_risk_fused(const Params& p, int t, hipStream_t s) {
+  if (p.noise == 1)
+    hipLaunchKernelGGL(k_mt_tab, dim3((p.Bt * p.H + 255) / 256), dim3(256), 0, s, p);
+  const int groups = (p.B + 63) / 64;
+  const size_t lds = size_t(2 * p.O * p.H + 2 * 64 * p.H) * 4;
+  hipLaunchKernelGGL(k_roll_cand, dim3((p.S + kRcWaves - 1) / kRcWaves, p.G * groups), dim3(64 * kRcWaves), lds, s,
+                     p, t);
+  const int threads = p.S >= 512 ? 512 : ((p.S + 63) / 64) * 64;
+  hipLaunchKernelGGL(k_risk_reduce, dim3(p.Bt), dim3(threads), risk_lds_bytes(p.O, p.H, p.S), s, p, t);
 }
 
 void launch_risk_baseline(const Params& p, int t, hipStream_t s) {

@@ -95,6 +95,8 @@ struct Params {
   uint32_t* bfix;          // [Bt*H*S] elements k_beta_planes deferred to k_beta_fix
   uint32_t* bfix_n;        // their count (zeroed by k_gamma_tab)
   double* gtab;            // [G][gamma_tab_size] Beta-noise attempt tables of the current iteration
+  void* mttab;             // [H][Bt] gamma constants per (step, candidate) of the fused rollouts (k_mt_tab)
+  float* rbar;             // [3][Bt][S] per-row maxima (collision, lane lb, ub) of the fused rollouts
   const float* beta_z0;    // [100][M+1]
   const float* beta_z;     // [20][pos_pad(M) * kBzCols] fp32 normals (bz_index layout, zero padded)
   // carry / state
@@ -223,6 +225,10 @@ void launch_noise(const Params& p, int t, hipStream_t s);
 void launch_front(const Params& p, int t, hipStream_t s);
 void launch_select(const Params& p, int t, hipStream_t s);
 void launch_risk_baseline(const Params& p, int t, hipStream_t s);
+// the same risk with candidate lanes and the Beta draws inside the rollouts
+// (k_mt_tab, k_roll_cand, k_risk_reduce); risk_fused(): the default path
+void launch_risk_fused(const Params& p, int t, hipStream_t s);
+bool risk_fused();
 
 // Monte-Carlo validation (k_validate.hip; S/validation.py:134-171)
 struct ValidateParams {

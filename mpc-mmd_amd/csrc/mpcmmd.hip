@@ -378,6 +378,8 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
       } else if (h->carla) {
         if (p.noise == MPCMMD_NOISE_BETA) h->launch(kKBetaPlanes, [&] { launch_beta_planes(p, t, h->stream); });
         run_carla_risk(h, t, 0);
+      } else if (risk_fused()) {
+        h->launch(kKRiskBaseline, [&] { launch_risk_fused(p, t, h->stream); });
       } else {
         if (p.noise == MPCMMD_NOISE_BETA) h->launch(kKBetaPlanes, [&] { launch_beta_planes(p, t, h->stream); });
         h->launch(kKRiskBaseline, [&] { launch_risk_baseline(p, t, h->stream); });
@@ -575,6 +577,8 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     p.bfix = (uint32_t*)h->alloc("bfix", c.noise == MPCMMD_NOISE_BETA ? BT * H * S * 4 : 16);
     p.bfix_n = (uint32_t*)h->alloc("bfix_n", 16);
     p.gtab = c.noise == MPCMMD_NOISE_BETA ? (double*)h->alloc("gtab", size_t(GM) * gamma_tab_size(S, H) * 8) : nullptr;
+    p.mttab = c.noise == MPCMMD_NOISE_BETA ? h->alloc("mttab", BT * H * 64) : nullptr;
+    p.rbar = (float*)h->alloc("rbar", size_t(3) * BT * S * 4);
     if (mmd_ok) {
       p.beta_z0 = (const float*)h->alloc("beta_z0", size_t(kBetaSamples) * (h->M + 1) * 4);
       p.beta_z = (const float*)h->alloc("beta_z", size_t(kBetaIters) * pos_pad(h->M) * kBzCols * 4);
