@@ -527,6 +527,10 @@ __global__ __launch_bounds__(64 * kRcWaves) void k_roll_cand(Params p, int t) {
                   k1, kStreamGammaSteerB, lg3, u3);
       n0 = beta_fused(fa, m.rinv.x, m.rinv.y, lg0, u0, lg1, u1);
       n1 = beta_fused(fs, m.rinv.z, m.rinv.w, lg2, u2, lg3, u3);
+      if (p.beta_dump && lane < nc) {  // parity tests: the draws as the [B][2][H][S] planes
+        p.bplane[b * 2 * HS + size_t(h) * S + r] = n0;
+        p.bplane[b * 2 * HS + HS + size_t(h) * S + r] = n1;
+      }
     }
     float an, sn;
     noisy_from(p, a, st, n0, n1, nc2, an, sn);
@@ -613,14 +617,6 @@ void launch_beta_planes(const Params& p, int t, hipStream_t s) {
 void launch_gamma_tab(const Params& p, int t, hipStream_t s) {
   const int total = kGammaTabStreams * kGammaTabAttempts * p.S * p.H;
   hipLaunchKernelGGL(k_gamma_tab, dim3((total + 255) / 256, p.G), dim3(256), 0, s, p, t);
-}
-
-bool risk_fused() {  // MPCMMD_RISK_FUSED=0: the row-lane rollouts over the Beta planes (A/B)
-  static const bool f = [] {
-    const char* e = std::getenv("MPCMMD_RISK_FUSED");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return f;
 }
 
 void launch_risk_fused(const Params& p, int t, hipStream_t s) {

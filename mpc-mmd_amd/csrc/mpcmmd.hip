@@ -378,7 +378,7 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
       } else if (h->carla) {
         if (p.noise == MPCMMD_NOISE_BETA) h->launch(kKBetaPlanes, [&] { launch_beta_planes(p, t, h->stream); });
         run_carla_risk(h, t, 0);
-      } else if (risk_fused()) {
+      } else if (!p.risk_rows) {
         h->launch(kKRiskBaseline, [&] { launch_risk_fused(p, t, h->stream); });
       } else {
         if (p.noise == MPCMMD_NOISE_BETA) h->launch(kKBetaPlanes, [&] { launch_beta_planes(p, t, h->stream); });
@@ -652,6 +652,8 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     if (BT >= 1024) h->groups = 2;
     h->groups_forced = std::getenv("MPCMMD_GROUPS") != nullptr;
     if (const char* g = std::getenv("MPCMMD_GRAPH")) h->graphs = std::atoi(g) != 0;
+    if (const char* g = std::getenv("MPCMMD_BETA_DUMP")) p.beta_dump = std::atoi(g) != 0;
+    if (const char* g = std::getenv("MPCMMD_RISK_FUSED")) p.risk_rows = std::atoi(g) == 0;
     if (const char* g = std::getenv("MPCMMD_GROUPS")) h->groups = std::max(1, std::min(mpcmmd_handle::kMaxGroups, std::atoi(g)));
     if (h->groups > 1) {
       HIPC(hipEventCreateWithFlags(&h->gev_start, hipEventDisableTiming));

@@ -91,9 +91,16 @@ def test_stage_lockstep(native, cost, noise):
 BETA_RTOL, BETA_ATOL = 1e-5, 3e-7
 
 
-def test_beta_planes(native):
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_beta_planes(native, monkeypatch, fused):
+    """The Beta draws of the baseline rollouts against the oracle's: the
+    fused rollouts (candidate lanes, draws inside the rollout; stored as
+    planes only under MPCMMD_BETA_DUMP for this test) and the row-lane plane
+    kernel (MPCMMD_RISK_FUSED=0)."""
     from oracle.rng import (STREAM_GAMMA_ACC_A, STREAM_GAMMA_ACC_B, STREAM_GAMMA_STEER_A, STREAM_GAMMA_STEER_B,
                             beta_draws, iteration_key)
+    monkeypatch.setenv("MPCMMD_BETA_DUMP", "1")   # read when the handle is created
+    monkeypatch.setenv("MPCMMD_RISK_FUSED", fused)
     ora, nat, xo, yo = make_pair(native, "cvar", "beta", n=N_S, O=O, H=H, B=B, T=T, acc_c=0.05, steer_c=0.01)
     draws = oracle.Draws.random(ora.prob, np.random.default_rng(3), idx_mpc=123, seed=0, with_beta_cem=False)
     nat.begin("cvar", 123, DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, xo, yo, 15.0, draws)
