@@ -388,57 +388,104 @@ __global__ __launch_bounds__(256) void k_beta_planes_c(Params p, int t) {
 struct MtTab {
   float4 c;      // c = 1 / sqrt(9 d) of the four gammas (acc a, acc b, steer a, steer b); NaN: control 0
   float4 l2d;    // log2 d
+  float4 d;      // d = alpha' - 1/3 (fp32 of the fp64 value)
+  float4 ctl;    // the controls: acc, steer (and two spare)
   double4 rinv;  // 1 / alpha where alpha < 1 (the boost), else 0: acc a, acc b, steer a, steer b
 };
+static_assert(sizeof(MtTab) == 96, "MtTab: 4 float4 + double4");
+// followed in Params::mttab by [H][Bt] double4: the fp64 c of the four gammas
+// (the exact v = 1 + c x of the rare paths)
 
 __global__ __launch_bounds__(256) void k_mt_tab(Params p) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (h, b): b fastest
   if (i >= p.Bt * p.H) return;
   const int h = i / p.Bt, b = i - h * p.Bt;
-  const float fa = fabsf(p.acc[size_t(b) * 100 + h]), fs = fabsf(p.steer[size_t(b) * 100 + h]);
+  const float ac = p.acc[size_t(b) * 100 + h], sc = p.steer[size_t(b) * 100 + h];
+  const float fa = fabsf(ac), fs = fabsf(sc);
   const double al[4] = {double(2.0f * fa), double(5.0f * fa), double(2.0f * fs), double(5.0f * fs)};
-  float c[4], l[4];
-  double r[4];
+  float c[4], l[4], d[4];
+  double r[4], c64[4];
   for (int k = 0; k < 4; ++k) {
     const MtConst m = mt_const(al[k]);
     c[k] = (k < 2 ? fa : fs) == 0.0f ? __int_as_float(0x7fc00000) : float(m.c);
     l[k] = __builtin_amdgcn_logf(float(m.d));
+    d[k] = float(m.d);
     r[k] = al[k] < 1.0 ? 1.0 / al[k] : 0.0;
+    c64[k] = m.c;
   }
   MtTab* o = reinterpret_cast<MtTab*>(p.mttab) + i;
   o->c = make_float4(c[0], c[1], c[2], c[3]);
   o->l2d = make_float4(l[0], l[1], l[2], l[3]);
+  o->d = make_float4(d[0], d[1], d[2], d[3]);
+  o->ctl = make_float4(ac, sc, 0.0f, 0.0f);
   o->rinv = double4{r[0], r[1], r[2], r[3]};
+  reinterpret_cast<double4*>(reinterpret_cast<MtTab*>(p.mttab) + size_t(p.Bt) * p.H)[i] =
+      double4{c64[0], c64[1], c64[2], c64[3]};
 }
 
-// One gamma of a Beta draw: attempt 0 in fp32 (tab0_fast's decisions), else
-// the fp64 table / Philox path of gamma_parts_tab from attempt 0 (the same
-// decisions again, then the later attempts).  Returns log2 G' and log U_boost.
-DEVI void gamma_fused(float c, float l2d, double alpha, double x, double lu, double lw, const double* tab, int S,
-                      int H, int r, int h, uint32_t k0, uint32_t k1, uint32_t stream, float& lg, double& lub) {
+// mt_log_test's fp32 test on v = vf, the fp32 v of the common path, for vf
+// >= 0.01.  With |eps| <= 2^-24 per rounding, vf = v + c x (e1 + e2 + e3) + v e4
+// and |c x| <= max(1, v - 1), so |vf - v| / v <= 2^-24 (3 max(1, v - 1) / v + 1):
+// at most 1.9e-5 at v = 0.01 and below 2.4e-7 for v >= 1.  An error e in v
+// moves rhs = q + d - d v^3 + d ln v^3 by 3 e (d v^3 + d), and the test's band
+// 1e-5 (1 + |lu| + q + d + d v^3 + |d ln v^3|) covers that with room (at
+// v = 0.01: 5.7e-5 d against at least 1.4e-4 d; for v >= 1, 7e-7 (d v^3 + d)
+// against 1e-5 (d v^3 + d)), so a decided result is the exact fp64 decision.
+// +1 accept, 0 reject, -1 undecided (the caller takes the exact path).
+DEVI int mt_log_test_vf(float xf, float luf, float df, float vf) {
+  const float v3f = vf * vf * vf;
+  const float q = 0.5f * xf * xf, dv = df * v3f, dl = df * (3.0f * __builtin_amdgcn_logf(vf) * 0.693147180559945309f);
+  const float rhs = ((q + df) - dv) + dl;
+  const float tol = 1e-5f * (1.0f + fabsf(luf) + q + fabsf(df) + fabsf(dv) + fabsf(dl));
+  if (luf < rhs - tol) return 1;
+  if (luf > rhs + tol) return 0;
+  return -1;
+}
+
+// One Marsaglia-Tsang attempt from a (wave-uniform) table entry (x, log u,
+// +-log w): v = 1 + c x in fp32 decides v > 0 unless it is within 1e-5 of 0
+// (then the fp64 v); the squeeze decision is the stored sign of log w; the log
+// test is mt_log_test on the fp64 v^3 (fp32 test, fp64 re-check).  The same
+// decisions as gamma_parts_tab's fp64 tab_try.  c64: the lane's fp64 c, loaded
+// only on those rare paths.  Returns log2 G' = log2 d + 3 log2 v and the boost
+// log-uniform when accepted.
+DEVI bool mt_try(float c, float l2d, double d, const double* c64, double x, double lu, double lw, float& lg,
+                 double& lub) {
   const float vf = 1.0f + c * float(x);
-  bool ok;
   float v = vf;
-  if (fabsf(vf) > 1e-5f) {
-    ok = vf > 0.0f;
-  } else {
-    const double vd = 1.0 + mt_const(alpha).c * x;
-    ok = vd > 0.0;
+  if (!(fabsf(vf) > 1e-5f)) {
+    const double vd = 1.0 + *c64 * x;
+    if (!(vd > 0.0)) return false;
     v = float(vd);
+    if (!(lw < 0.0) && !mt_log_test(x, lu, d, vd * vd * vd)) return false;
+  } else {
+    if (!(vf > 0.0f)) return false;
+    if (!(lw < 0.0)) {  // the squeeze rejected (wave-uniform): the exact log test
+      const double vd = 1.0 + *c64 * x;
+      if (!mt_log_test(x, lu, d, vd * vd * vd)) return false;
+    }
   }
-  if (ok && !(lw < 0.0)) {  // the squeeze rejected: the exact log test
-    const MtConst m = mt_const(alpha);
-    const double vd = 1.0 + m.c * x;
-    ok = mt_log_test(x, lu, m.d, vd * vd * vd);
+  lg = l2d + 3.0f * __builtin_amdgcn_logf(v);
+  lub = -fabs(lw);
+  return true;
+}
+
+// One gamma by the exact path: the table's attempts from 0 (mt_try, the
+// exact decisions), then the full fp64 sampler for longer chains (about one
+// gamma in 10^6).  tab: this stream's table at (attempt 0, h, r).
+DEVI void gamma_exact(float c, float l2d, double alpha, const double* c64, const double* tab, size_t plane, int S,
+                      int H, int r, int h, uint32_t k0, uint32_t k1, uint32_t stream, float& lg, double& lub) {
+  const double d = (alpha < 1.0 ? alpha + 1.0 : alpha) - 1.0 / 3.0;  // mt_const's d
+#pragma unroll 1
+  for (int a = 0; a < kGammaTabAttempts; ++a) {
+    const double* e = tab + size_t(a) * 4 * plane;
+    if (mt_try(c, l2d, d, c64, e[0], e[2 * plane], e[3 * plane], lg, lub)) return;
   }
-  if (ok) {
-    lg = l2d + 3.0f * __builtin_amdgcn_logf(v);
-    lub = -fabs(lw);
-    return;
-  }
-  double g;
-  gamma_parts_tab(mt_const(alpha), tab, S, H, r, h, k0, k1, stream, uint32_t(r) * uint32_t(H) + uint32_t(h), g, lub);
-  lg = __builtin_amdgcn_logf(float(g));
+  const size_t at = size_t(h) * S + r;
+  double gg;
+  gamma_parts_tab(mt_const(alpha), tab - at, S, H, r, h, k0, k1, stream, uint32_t(r) * uint32_t(H) + uint32_t(h), gg,
+                  lub);
+  lg = __builtin_amdgcn_logf(float(gg));
 }
 
 DEVI float beta_fused(float fabs_ctl, double ra, double rb, float lga, double ua, float lgb, double ub) {
@@ -448,94 +495,162 @@ DEVI float beta_fused(float fabs_ctl, double ra, double rb, float lga, double ua
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(d));
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// f_bar (compute_f_bar, costs.py:50-60) of two obstacles at once in packed
+// fp32 (v_pk_*: the same IEEE roundings as f_bar, two lanes per instruction)
+DEVI f2v f_bar2(float x, float y, f2v xo, f2v yo) {
+  constexpr float kA2 = 18.0625f, kB2 = 7.5625f;
+  const f2v wc = f2v{x, x} - xo, ws = f2v{y, y} - yo;
+  const f2v a = wc * wc, b = ws * ws;
+  const f2v ra = f2v{1.0f / kA2, 1.0f / kA2}, rb = f2v{1.0f / kB2, 1.0f / kB2};
+  const f2v qa = a * ra, qb = b * rb;  // div_rc(x, d, r): q + (x - q d) r
+  const f2v ea = __builtin_elementwise_fma(-qa, f2v{kA2, kA2}, a), eb = __builtin_elementwise_fma(-qb, f2v{kB2, kB2}, b);
+  const f2v da = __builtin_elementwise_fma(ea, ra, qa), db = __builtin_elementwise_fma(eb, rb, qb);
+  return (-da - db) + f2v{1.0f, 1.0f};
+}
+
 constexpr int kRcWaves = 4;
 
+// attempt 0 of one gamma stream at (row, step), staged in LDS: x and log u in
+// fp32 (the common path's operands), +-log w in fp64 (the boost log-uniform)
+struct Tab0 {
+  float xf, luf;
+  double lw;
+};
+
+// One gamma by the fp32 common path: attempt 0 from LDS, attempts 1.. from
+// the table in global memory (wave-uniform entries).  false: an attempt the
+// fp32 tests cannot decide, or all tabulated attempts rejected -- the caller
+// takes the exact path (gamma_exact).
+DEVI bool gamma_fast(float c, float l2d, float df, const Tab0& e0, const double* tab, size_t plane, float& lg,
+                     double& lub) {
+  float xf = e0.xf, luf = e0.luf;
+  double lw = e0.lw;
+  for (int a = 0;;) {
+    const float vf = 1.0f + c * xf;
+    int dec;  // 1 accept, 0 reject, -1 undecided
+    if (!(fabsf(vf) > 1e-5f)) {
+      dec = -1;  // also NaN c (control 0)
+    } else if (!(vf > 0.0f)) {
+      dec = 0;
+    } else if (lw < 0.0) {
+      dec = 1;  // the squeeze accepted
+    } else {
+      dec = vf >= 0.01f ? mt_log_test_vf(xf, luf, df, vf) : -1;
+    }
+    if (dec == 1) {
+      lg = l2d + 3.0f * __builtin_amdgcn_logf(vf);
+      lub = -fabs(lw);
+      return true;
+    }
+    if (dec < 0 || ++a == kGammaTabAttempts) return false;
+    const double* e = tab + size_t(a) * 4 * plane;
+    xf = float(e[0]);
+    luf = float(e[2 * plane]);
+    lw = e[3 * plane];
+  }
+}
+
+// Fused baseline rollouts (see above): per step the four gammas by the fp32
+// common path (gamma_fast; attempt 0 staged in LDS), a gamma it cannot
+// decide by the exact path (gamma_exact), the Beta draws, then the rollout
+// step; nothing but the per-row maxima leaves the kernel.
 __global__ __launch_bounds__(64 * kRcWaves) void k_roll_cand(Params p, int t) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int S = p.S, H = p.H, O = p.O;
+  const int S = p.S, H = p.H, O = p.O, Op = (O + 1) & ~1;  // obstacles padded to pairs
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int groups = (p.B + 63) / 64;
   const int g = blockIdx.y / groups, j0 = (blockIdx.y - g * groups) * 64;
   const int nc = min(64, p.B - j0);
+  const int r0 = blockIdx.x * kRcWaves, nr = min(kRcWaves, S - r0);
   const Cfg cf = cfg_of(p, g);
-  float* xo = reinterpret_cast<float*>(smem);
-  float* yo = xo + O * H;
-  float* ca = yo + O * H;  // [H][64] controls of the block's candidates
-  float* cs = ca + 64 * H;
-  for (int i = threadIdx.x; i < O * H; i += blockDim.x) {
-    xo[i] = cf.obs[i];
-    yo[i] = cf.obs[O * H + i];
+  const bool beta = p.noise == 1;
+  const size_t HS = size_t(H) * S;
+  const size_t plane = HS, sl = size_t(kGammaTabAttempts) * 4 * plane;
+  f2v* ob = reinterpret_cast<f2v*>(smem);                  // [H][Op/2] x pairs, then y pairs
+  Tab0* t0 = reinterpret_cast<Tab0*>(ob + H * Op);         // [kRcWaves][H][4 streams]
+  for (int i = threadIdx.x; i < Op * H; i += blockDim.x) {  // transpose [O][H] -> [H][O]; a pad repeats obstacle 0
+    const int h = i / Op, o = i - h * Op, os = o < O ? o : 0;
+    reinterpret_cast<float*>(ob)[i] = cf.obs[os * H + h];
+    reinterpret_cast<float*>(ob + (H * Op) / 2)[i] = cf.obs[O * H + os * H + h];
   }
-  for (int i = threadIdx.x; i < 64 * H; i += blockDim.x) {
-    const int h = i >> 6, cl = min(i & 63, nc - 1);
-    const size_t bb = size_t(g) * p.B + j0 + cl;
-    ca[i] = p.acc[bb * 100 + h];
-    cs[i] = p.steer[bb * 100 + h];
+  if (beta) {
+    for (int i = threadIdx.x; i < kRcWaves * H * 4; i += blockDim.x) {  // (row, step, stream), stream fastest
+      const int k = i & 3, wh = i >> 2, rw = wh / H, h = wh - rw * H;
+      const double* e = cf.gtab + k * sl + size_t(h) * S + r0 + min(rw, nr - 1);
+      t0[i] = Tab0{float(e[0]), float(e[2 * plane]), e[3 * plane]};
+    }
   }
   __syncthreads();
-  const int r = blockIdx.x * kRcWaves + w;
-  if (r >= S) return;
+  const int r = r0 + w;
+  if (w >= nr) return;
   const int c = min(lane, nc - 1);
   const size_t b = size_t(g) * p.B + j0 + c;
-  const size_t HS = size_t(H) * S;
   const float* rl = cf.roll + size_t(t) * 3 * HS + r;  // [3][H][S]: uniform per wave
-  const bool beta = p.noise == 1;
-  const double* gt = beta ? cf.gtab : nullptr;
-  const size_t plane = HS, sl = size_t(kGammaTabAttempts) * 4 * plane;
+  const double* gt = beta ? cf.gtab + size_t(r) : nullptr;  // + h S + k sl + a 4 plane + field plane
   const uint32_t k0 = iteration_key0(cf.idx_mpc, t), k1 = p.seed;
   const MtTab* mt = reinterpret_cast<const MtTab*>(p.mttab);
+  const double* mc64 = reinterpret_cast<const double*>(mt + size_t(p.Bt) * H);
+  const Tab0* tw = t0 + w * H * 4;
+  const f2v* obx = ob;
+  const f2v* oby = ob + (H * Op) / 2;
+  const int Op2 = Op / 2;
   float x = cf.st0[0], y = cf.st0[1], vx = cf.st0[2], vy = cf.st0[3], psi = cf.st0[4];
   float cb = 0.0f, lb = 0.0f, ub = 0.0f;
+  f2v nsum = f2v{0.0f, 0.0f};  // sum of every f_bar: NaN iff one is (f_bar <= 1, never +inf)
   bool nan = false;
   for (int h = 0; h < H; ++h) {
-    for (int o = 0; o < O; ++o) {  // k_risk_baseline's residual (skip where f_bar <= 0 is certain)
-      const float xov = xo[o * H + h];
-      if (!(fabsf(x - xov) >= kObsA)) {
-        const float cc = f_bar(x, y, xov, yo[o * H + h]);
-        nan |= (cc != cc);
-        cb = fmaxf(cb, cc);
-      }
+    for (int o = 0; o < Op2; ++o) {  // k_risk_baseline's residual max over the obstacles, two at a time
+      const f2v cc = f_bar2(x, y, obx[h * Op2 + o], oby[h * Op2 + o]);
+      nsum += cc;
+      cb = fmaxf(cb, fmaxf(cc.x, cc.y));
     }
     const float l1 = -y + p.y_lb, u1 = y - p.y_ub;
     nan |= (y != y) | (x != x);
     lb = fmaxf(lb, l1);
     ub = fmaxf(ub, u1);
-    if (h == H - 1) break;
-    const float a = ca[h * 64 + lane], st = cs[h * 64 + lane];
+    if (h == H - 1 && !p.beta_dump) break;  // the last step's draw moves nothing (dumped for the tests only)
     const float nc2 = rl[2 * HS + size_t(h) * S];
-    float n0, n1;
+    float a, st, n0, n1;
     if (!beta) {
+      a = p.acc[b * 100 + h];
+      st = p.steer[b * 100 + h];
       n0 = rl[size_t(h) * S];
       n1 = rl[HS + size_t(h) * S];
     } else {
-      const MtTab m = mt[size_t(h) * p.Bt + b];
-      const size_t at = size_t(h) * S + r;
-      const double* e0 = gt + at;
-      const double* e1 = gt + sl + at;
-      const double* e2 = gt + 2 * sl + at;
-      const double* e3 = gt + 3 * sl + at;
-      const float fa = fabsf(a), fs = fabsf(st);
-      float lg0, lg1, lg2, lg3;
-      double u0, u1, u2, u3;
-      gamma_fused(m.c.x, m.l2d.x, double(2.0f * fa), e0[0], e0[2 * plane], e0[3 * plane], gt, S, H, r, h, k0, k1,
-                  kStreamGammaAccA, lg0, u0);
-      gamma_fused(m.c.y, m.l2d.y, double(5.0f * fa), e1[0], e1[2 * plane], e1[3 * plane], gt + sl, S, H, r, h, k0,
-                  k1, kStreamGammaAccB, lg1, u1);
-      gamma_fused(m.c.z, m.l2d.z, double(2.0f * fs), e2[0], e2[2 * plane], e2[3 * plane], gt + 2 * sl, S, H, r, h, k0,
-                  k1, kStreamGammaSteerA, lg2, u2);
-      gamma_fused(m.c.w, m.l2d.w, double(5.0f * fs), e3[0], e3[2 * plane], e3[3 * plane], gt + 3 * sl, S, H, r, h, k0,
-                  k1, kStreamGammaSteerB, lg3, u3);
-      n0 = beta_fused(fa, m.rinv.x, m.rinv.y, lg0, u0, lg1, u1);
-      n1 = beta_fused(fs, m.rinv.z, m.rinv.w, lg2, u2, lg3, u3);
+      const size_t hb = size_t(h) * p.Bt + b;
+      const MtTab m = mt[hb];
+      a = m.ctl.x;
+      st = m.ctl.y;
+      const double* e = gt + size_t(h) * S;
+      const float cv[4] = {m.c.x, m.c.y, m.c.z, m.c.w}, lv[4] = {m.l2d.x, m.l2d.y, m.l2d.z, m.l2d.w};
+      const float dv[4] = {m.d.x, m.d.y, m.d.z, m.d.w};
+      float lg[4];
+      double ug[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // the fp32 common path, else the exact path
+        if (!gamma_fast(cv[k], lv[k], dv[k], tw[h * 4 + k], e + k * sl, plane, lg[k], ug[k])) {
+          const double alpha = double(((k & 1) ? 5.0f : 2.0f) * fabsf(k < 2 ? a : st));
+          const uint32_t stream = k == 0 ? kStreamGammaAccA : k == 1 ? kStreamGammaAccB : k == 2 ? kStreamGammaSteerA
+                                                                                                 : kStreamGammaSteerB;
+          gamma_exact(cv[k], lv[k], alpha, mc64 + 4 * hb + k, e + k * sl, plane, S, H, r, h, k0, k1, stream, lg[k],
+                      ug[k]);
+        }
+      }
+      n0 = beta_fused(fabsf(a), m.rinv.x, m.rinv.y, lg[0], ug[0], lg[1], ug[1]);
+      n1 = beta_fused(fabsf(st), m.rinv.z, m.rinv.w, lg[2], ug[2], lg[3], ug[3]);
       if (p.beta_dump && lane < nc) {  // parity tests: the draws as the [B][2][H][S] planes
         p.bplane[b * 2 * HS + size_t(h) * S + r] = n0;
         p.bplane[b * 2 * HS + HS + size_t(h) * S + r] = n1;
       }
     }
+    if (h == H - 1) break;
     float an, sn;
     noisy_from(p, a, st, n0, n1, nc2, an, sn);
     bicycle_step(x, y, vx, vy, psi, an, sn);
   }
+  nan |= (nsum.x != nsum.x) | (nsum.y != nsum.y);
   if (lane < nc) {
     const float qnan = __int_as_float(0x7fc00000);
     const size_t bs = size_t(p.Bt) * S;
@@ -619,11 +734,13 @@ void launch_gamma_tab(const Params& p, int t, hipStream_t s) {
   hipLaunchKernelGGL(k_gamma_tab, dim3((total + 255) / 256, p.G), dim3(256), 0, s, p, t);
 }
 
+size_t mt_tab_entry_bytes() { return sizeof(MtTab) + sizeof(double4); }
+
 void launch_risk_fused(const Params& p, int t, hipStream_t s) {
   if (p.noise == 1)
     hipLaunchKernelGGL(k_mt_tab, dim3((p.Bt * p.H + 255) / 256), dim3(256), 0, s, p);
   const int groups = (p.B + 63) / 64;
-  const size_t lds = size_t(2 * p.O * p.H + 2 * 64 * p.H) * 4;
+  const size_t lds = size_t(2 * ((p.O + 1) & ~1) * p.H) * 4 + (p.noise == 1 ? sizeof(Tab0) * kRcWaves * p.H * 4 : 0);
   hipLaunchKernelGGL(k_roll_cand, dim3((p.S + kRcWaves - 1) / kRcWaves, p.G * groups), dim3(64 * kRcWaves), lds, s,
                      p, t);
   const int threads = p.S >= 512 ? 512 : ((p.S + 63) / 64) * 64;

@@ -98,7 +98,7 @@ struct Params {
   void* mttab;             // [H][Bt] gamma constants per (step, candidate) of the fused rollouts (k_mt_tab)
   float* rbar;             // [3][Bt][S] per-row maxima (collision, lane lb, ub) of the fused rollouts
   int32_t beta_dump;       // fused rollouts also store their Beta draws in bplane (MPCMMD_BETA_DUMP, tests)
-  int32_t risk_rows;       // 1: the row-lane rollouts over Beta planes (MPCMMD_RISK_FUSED=0 at create, A/B)
+  int32_t risk_rows;       // 1 (default): the row-lane rollouts over Beta planes; 0: fused (MPCMMD_RISK_FUSED=1)
   const float* beta_z0;    // [100][M+1]
   const float* beta_z;     // [20][pos_pad(M) * kBzCols] fp32 normals (bz_index layout, zero padded)
   // carry / state
@@ -228,8 +228,9 @@ void launch_front(const Params& p, int t, hipStream_t s);
 void launch_select(const Params& p, int t, hipStream_t s);
 void launch_risk_baseline(const Params& p, int t, hipStream_t s);
 // the same risk with candidate lanes and the Beta draws inside the rollouts
-// (k_mt_tab, k_roll_cand, k_risk_reduce): the default path (Params::risk_rows = 0)
+// (k_mt_tab, k_roll_cand, k_risk_reduce): Params::risk_rows = 0 (MPCMMD_RISK_FUSED=1)
 void launch_risk_fused(const Params& p, int t, hipStream_t s);
+size_t mt_tab_entry_bytes();  // Params::mttab bytes per (step, candidate)
 
 // Monte-Carlo validation (k_validate.hip; S/validation.py:134-171)
 struct ValidateParams {

@@ -577,7 +577,7 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     p.bfix = (uint32_t*)h->alloc("bfix", c.noise == MPCMMD_NOISE_BETA ? BT * H * S * 4 : 16);
     p.bfix_n = (uint32_t*)h->alloc("bfix_n", 16);
     p.gtab = c.noise == MPCMMD_NOISE_BETA ? (double*)h->alloc("gtab", size_t(GM) * gamma_tab_size(S, H) * 8) : nullptr;
-    p.mttab = c.noise == MPCMMD_NOISE_BETA ? h->alloc("mttab", BT * H * 64) : nullptr;
+    p.mttab = c.noise == MPCMMD_NOISE_BETA ? h->alloc("mttab", BT * H * mt_tab_entry_bytes()) : nullptr;
     p.rbar = (float*)h->alloc("rbar", size_t(3) * BT * S * 4);
     if (mmd_ok) {
       p.beta_z0 = (const float*)h->alloc("beta_z0", size_t(kBetaSamples) * (h->M + 1) * 4);
@@ -653,6 +653,7 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     h->groups_forced = std::getenv("MPCMMD_GROUPS") != nullptr;
     if (const char* g = std::getenv("MPCMMD_GRAPH")) h->graphs = std::atoi(g) != 0;
     if (const char* g = std::getenv("MPCMMD_BETA_DUMP")) p.beta_dump = std::atoi(g) != 0;
+    p.risk_rows = 1;  // the row-lane path is the faster one at configs[2]; MPCMMD_RISK_FUSED=1: fused
     if (const char* g = std::getenv("MPCMMD_RISK_FUSED")) p.risk_rows = std::atoi(g) == 0;
     if (const char* g = std::getenv("MPCMMD_GROUPS")) h->groups = std::max(1, std::min(mpcmmd_handle::kMaxGroups, std::atoi(g)));
     if (h->groups > 1) {
