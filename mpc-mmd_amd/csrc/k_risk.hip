@@ -244,55 +244,80 @@ __global__ __launch_bounds__(256) void k_beta_planes(Params p, int t) {
   }
 }
 
-// The same draws with one lane per CANDIDATE (64 candidates of one
-// configuration) and a wave walking 16 rows of one step: the attempt-table
-// entry of a (row, step) is then one value for the whole wave (scalar loads),
-// so the alpha-independent squeeze decision -- which decides whether the fp32 /
-// fp64 log test and the later attempts run at all -- is wave-uniform, and a
-// wave executes those rare paths only where its (row, step) needs them
-// instead of whenever any of its 64 rows does (row lanes: nearly always).
-// Per lane the alpha-dependent transforms and the combine are the identical
-// functions of k_beta_planes (bit-identical draws).  The [64 rows][64
-// candidates] tile goes through LDS so the planes are stored as 256-byte row
-// runs per candidate.
-constexpr int kBpRows = 64;
+// mt_log_test's fp32 test on v = vp, the common path's fp32 v to within two
+// ulp (v_precise): an error e <= 2.4e-7 relative in v moves rhs = q + d - d v^3
+// + d ln v^3 by at most 3 e (d v^3 + d) + fp32 rounding of the terms, far inside
+// the test's band 1e-5 (1 + |lu| + q + d + d v^3 + |d ln v^3|), so a decided
+// result is the exact fp64 decision.  +1 accept, 0 reject, -1 undecided (the
+// caller takes the exact path).
+DEVI int mt_log_test_vf(float xf, float luf, float df, float vp) {
+  const float v3f = vp * vp * vp;
+  const float q = 0.5f * xf * xf, dv = df * v3f, dl = df * (3.0f * __builtin_amdgcn_logf(vp) * 0.693147180559945309f);
+  const float rhs = ((q + df) - dv) + dl;
+  const float tol = 1e-5f * (1.0f + fabsf(luf) + q + fabsf(df) + fabsf(dv) + fabsf(dl));
+  if (luf < rhs - tol) return 1;
+  if (luf > rhs + tol) return 0;
+  return -1;
+}
 
-// Per lane (candidate) and gamma stream: the Marsaglia-Tsang constants in
-// fp64 (the exact decisions, fallbacks) and the fp32 forms of the common path.
-struct MtLane {
-  MtConst m;
-  float c, log2d;
+// v = 1 + c x to within two fp32 ulp for any v >> 1e-13, from the fp32 pairs
+// c = c + clo, x = xf + xlo (the fp64 values split): c xf = ph + pl exactly
+// (fma), 1 + ph = s + e1 exactly (two-sum); the small terms added once.
+DEVI float v_precise(float c, float clo, float xf, float xlo) {
+  const float ph = c * xf;
+  const float pl = fmaf(c, xf, -ph);
+  const float s = 1.0f + ph;
+  const float bb = s - 1.0f;
+  const float e1 = (1.0f - (s - bb)) + (ph - bb);
+  return s + (e1 + (pl + (c * xlo + clo * xf)));
+}
+
+// attempt 0 of one gamma stream at (row, step), staged in LDS: x as an fp32
+// pair and log u in fp32 (the common path's operands), +-log w in fp64 (the
+// boost log-uniform)
+struct Tab0 {
+  float xf, xlo, luf;
+  double lw;
 };
-DEVI MtLane mt_lane(double alpha) {
-  const MtConst m = mt_const(alpha);
-  return MtLane{m, float(m.c), __builtin_amdgcn_logf(float(m.d))};
+DEVI Tab0 tab0_of(const double* e, size_t plane) {
+  const double x = e[0];
+  const float xf = float(x);
+  return Tab0{xf, float(x - double(xf)), float(e[2 * plane]), e[3 * plane]};
 }
 
-// Attempt 0 of one gamma from the staged table entry (x, log u, +-log w):
-// the fp32 common path.  v = 1 + c x in fp32 decides v > 0 unless it is
-// within 1e-5 of 0 (then fp64, the exact test); the squeeze decision is the
-// stored sign of log w (wave-uniform); the log test is mt_log_test's fp32
-// test with its fp64 re-check.  Returns log2 G' = log2 d + 3 log2 v (fp32)
-// and the boost log-uniform; false = rejected (attempts 1.. follow).
-DEVI bool tab0_fast(const MtLane& L, double x, double lu, double lw, float& lg, double& lub) {
-  const float xf = float(x);
-  const float vf = 1.0f + L.c * xf;
-  float v = vf;
-  if (!(fabsf(vf) > 1e-5f)) {
-    const double vd = 1.0 + L.m.c * x;
-    if (!(vd > 0.0)) return false;
-    v = float(vd);
-  } else if (!(vf > 0.0f)) {
-    return false;
+// One gamma by the fp32 common path: attempt 0 from LDS, attempts 1.. from
+// the table in global memory (wave-uniform entries); c, clo: the fp32 pair of
+// the gamma's c.  v = 1 + c x is formed in plain fp32 first; where the squeeze
+// rejected (the log test follows) or v < 0.5 (log2 v carries into the draw),
+// v_precise replaces it.  |v| <= 1e-5 (its sign in doubt), a log test inside
+// its band, or more attempts than tabulated: false -- the caller takes the
+// exact path.
+DEVI bool gamma_fast(float c, float clo, float l2d, float df, const Tab0& e0, const double* tab, size_t plane,
+                     float& lg, double& lub) {
+  Tab0 e = e0;
+  for (int a = 0;;) {
+    const float vf = 1.0f + c * e.xf;
+    int dec;  // 1 accept, 0 reject, -1 undecided
+    float v = vf;
+    if (!(fabsf(vf) > 1e-5f)) {
+      dec = -1;
+    } else if (!(vf > 0.0f)) {
+      dec = 0;
+    } else {
+      if (!(e.lw < 0.0) || vf < 0.5f) v = v_precise(c, clo, e.xf, e.xlo);
+      dec = e.lw < 0.0 ? 1 : mt_log_test_vf(e.xf, e.luf, df, v);  // lw < 0: the squeeze accepted
+    }
+    if (dec == 1) {
+      lg = l2d + 3.0f * __builtin_amdgcn_logf(v);
+      lub = -fabs(e.lw);
+      return true;
+    }
+    if (dec < 0 || ++a == kGammaTabAttempts) return false;
+    e = tab0_of(tab + size_t(a) * 4 * plane, plane);
   }
-  if (!(lw < 0.0)) {  // the squeeze rejected: the log test on v^3
-    const double vd = 1.0 + L.m.c * x;
-    if (!mt_log_test(x, lu, L.m.d, vd * vd * vd)) return false;
-  }
-  lg = L.log2d + 3.0f * __builtin_amdgcn_logf(v);
-  lub = -fabs(lw);
-  return true;
 }
+
+constexpr int kBpRows = 32;  // rows per k_beta_planes_c workgroup (8 per wave)
 
 // Beta(a, b) = 1 / (1 + 2^(log2 Gb - log2 Ga)) from the gammas' log2 G' and
 // boost log-uniforms (beta_combine's formula, the log2 G' given).
@@ -309,14 +334,16 @@ DEVI float beta_from_logs(double a, double b, double ra, double rb, float lga, d
 }
 
 // The same draws with one lane per CANDIDATE (64 candidates of one
-// configuration) and a wave walking 16 rows of one step: the attempt-table
+// configuration) and a wave walking 8 rows of one step: the attempt-table
 // entry of a (row, step) is one value for the whole wave, so the
 // alpha-independent squeeze decision -- which decides whether the log test
-// runs at all -- is wave-uniform.  The workgroup's 64 rows of attempt 0 are
-// staged in LDS (one coalesced pass); attempt 0 runs the fp32 common path
-// (tab0_fast), rejected attempts the fp64 table path of k_beta_planes,
-// longer chains go to k_beta_fix.  The [64 rows][64 candidates] result tile
-// goes through LDS so the planes are stored as 256-byte row runs.
+// runs at all -- is wave-uniform (row lanes would take the rare paths whenever
+// any of their 64 rows does).  Attempt 0 of the workgroup's rows is staged in
+// LDS (one coalesced pass); every gamma runs the fp32 common path (gamma_fast,
+// later attempts from global memory); an element it cannot decide (about 4
+// in 10^4) goes to k_beta_fix, the full fp64 sampler.  The [32 rows][64
+// candidates] result tile goes through LDS so the planes are stored as
+// 128-byte row runs per candidate.
 __global__ __launch_bounds__(256) void k_beta_planes_c(Params p, int t) {
   const int S = p.S, H = p.H;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -326,40 +353,42 @@ __global__ __launch_bounds__(256) void k_beta_planes_c(Params p, int t) {
   const int nc = min(64, p.B - j0), nr = min(kBpRows, S - r0);
   const double* gt = p.gtab + size_t(g) * gtab_stride(S, H);
   const size_t plane = size_t(S) * H, sl = size_t(kGammaTabAttempts) * 4 * plane;
-  __shared__ double t0x[4][kBpRows], t0u[4][kBpRows], t0w[4][kBpRows];
+  __shared__ Tab0 t0[4][kBpRows];
   __shared__ float tile[2][kBpRows][65];
   for (int q = threadIdx.x; q < 4 * kBpRows; q += blockDim.x) {  // attempt 0, streams acc A/B, steer A/B
     const int k = q / kBpRows, rl = q - k * kBpRows;
     const double* e = gt + k * sl + size_t(h) * S + r0 + min(rl, nr - 1);
-    t0x[k][rl] = e[0];
-    t0u[k][rl] = e[2 * plane];
-    t0w[k][rl] = e[3 * plane];
+    t0[k][rl] = tab0_of(e, plane);
   }
   const int c = min(lane, nc - 1);
   const uint32_t b = uint32_t(g) * p.B + j0 + c;
   const float fa = fabsf(p.acc[size_t(b) * 100 + h]), fs = fabsf(p.steer[size_t(b) * 100 + h]);
   const double aa = double(2.0f * fa), ab = double(5.0f * fa), sa = double(2.0f * fs), sb = double(5.0f * fs);
-  const MtLane L[4] = {mt_lane(aa), mt_lane(ab), mt_lane(sa), mt_lane(sb)};
+  const double al[4] = {aa, ab, sa, sb};
+  float cv[4], cl[4], lv[4], dv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // the gammas' constants (k_mt_tab's)
+    const MtConst m = mt_const(al[k]);
+    cv[k] = float(m.c);
+    cl[k] = float(m.c - double(cv[k]));
+    lv[k] = __builtin_amdgcn_logf(float(m.d));
+    dv[k] = float(m.d);
+  }
   __syncthreads();
   for (int i = 0; i < kBpRows / 4; ++i) {
     const int rl = w * (kBpRows / 4) + i, r = r0 + rl;
     if (rl >= nr) break;
-    const size_t at = size_t(h) * S + r;
-    // one gamma: the fp32 attempt 0, else the fp64 table attempts 1..3
-    auto gam = [&](int k, float& lg, double& lub) {
-      if (tab0_fast(L[k], t0x[k][rl], t0u[k][rl], t0w[k][rl], lg, lub)) return true;
-      double gg;
-      if (!gamma_tab_from(L[k].m, gt + k * sl, plane, at, 1, gg, lub)) return false;
-      lg = __builtin_amdgcn_logf(float(gg));
-      return true;
-    };
-    float lg0, lg1, lg2, lg3;
-    double u0, u1, u2, u3;
-    const bool ok = gam(0, lg0, u0) && gam(1, lg1, u1) && gam(2, lg2, u2) && gam(3, lg3, u3);
+    const double* e = gt + size_t(h) * S + r;
+    float lg[4];
+    double ug[4];
+    int ok = 1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      ok &= int(gamma_fast(cv[k], cl[k], lv[k], dv[k], t0[k][rl], e + k * sl, plane, lg[k], ug[k]));
     if (ok) {
-      tile[0][rl][lane] = beta_from_logs(aa, ab, 2.0, 5.0, lg0, u0, lg1, u1);
-      tile[1][rl][lane] = beta_from_logs(sa, sb, 2.0, 5.0, lg2, u2, lg3, u3);
-    } else if (lane < nc) {  // more attempts than tabulated: k_beta_fix (after this launch) writes it
+      tile[0][rl][lane] = beta_from_logs(aa, ab, 2.0, 5.0, lg[0], ug[0], lg[1], ug[1]);
+      tile[1][rl][lane] = beta_from_logs(sa, sb, 2.0, 5.0, lg[2], ug[2], lg[3], ug[3]);
+    } else if (lane < nc) {  // undecided in fp32 or more attempts than tabulated: k_beta_fix writes it
       const unsigned slot = atomicAdd(p.bfix_n, 1u);
       p.bfix[slot] = (b * uint32_t(H) + uint32_t(h)) * uint32_t(S) + uint32_t(r);
     }
@@ -386,13 +415,14 @@ __global__ __launch_bounds__(256) void k_beta_planes_c(Params p, int t) {
 // are k_risk_baseline's arithmetic; the per-row maxima go to Params::rbar and
 // k_risk_reduce applies the reducer (one workgroup per candidate).
 struct MtTab {
-  float4 c;      // c = 1 / sqrt(9 d) of the four gammas (acc a, acc b, steer a, steer b); NaN: control 0
+  float4 c;      // c = 1 / sqrt(9 d) of the four gammas (acc a, acc b, steer a, steer b)
   float4 l2d;    // log2 d
   float4 d;      // d = alpha' - 1/3 (fp32 of the fp64 value)
   float4 ctl;    // the controls: acc, steer (and two spare)
+  float4 clo;    // c - float(c) (the fp32 pair of c, v_precise)
   double4 rinv;  // 1 / alpha where alpha < 1 (the boost), else 0: acc a, acc b, steer a, steer b
 };
-static_assert(sizeof(MtTab) == 96, "MtTab: 4 float4 + double4");
+static_assert(sizeof(MtTab) == 128, "MtTab: 5 float4 + double4 (32-byte aligned)");
 // followed in Params::mttab by [H][Bt] double4: the fp64 c of the four gammas
 // (the exact v = 1 + c x of the rare paths)
 
@@ -403,11 +433,12 @@ __global__ __launch_bounds__(256) void k_mt_tab(Params p) {
   const float ac = p.acc[size_t(b) * 100 + h], sc = p.steer[size_t(b) * 100 + h];
   const float fa = fabsf(ac), fs = fabsf(sc);
   const double al[4] = {double(2.0f * fa), double(5.0f * fa), double(2.0f * fs), double(5.0f * fs)};
-  float c[4], l[4], d[4];
+  float c[4], l[4], d[4], cl[4];
   double r[4], c64[4];
   for (int k = 0; k < 4; ++k) {
     const MtConst m = mt_const(al[k]);
-    c[k] = (k < 2 ? fa : fs) == 0.0f ? __int_as_float(0x7fc00000) : float(m.c);
+    c[k] = float(m.c);
+    cl[k] = float(m.c - double(c[k]));
     l[k] = __builtin_amdgcn_logf(float(m.d));
     d[k] = float(m.d);
     r[k] = al[k] < 1.0 ? 1.0 / al[k] : 0.0;
@@ -418,28 +449,10 @@ __global__ __launch_bounds__(256) void k_mt_tab(Params p) {
   o->l2d = make_float4(l[0], l[1], l[2], l[3]);
   o->d = make_float4(d[0], d[1], d[2], d[3]);
   o->ctl = make_float4(ac, sc, 0.0f, 0.0f);
+  o->clo = make_float4(cl[0], cl[1], cl[2], cl[3]);
   o->rinv = double4{r[0], r[1], r[2], r[3]};
   reinterpret_cast<double4*>(reinterpret_cast<MtTab*>(p.mttab) + size_t(p.Bt) * p.H)[i] =
       double4{c64[0], c64[1], c64[2], c64[3]};
-}
-
-// mt_log_test's fp32 test on v = vf, the fp32 v of the common path, for vf
-// >= 0.01.  With |eps| <= 2^-24 per rounding, vf = v + c x (e1 + e2 + e3) + v e4
-// and |c x| <= max(1, v - 1), so |vf - v| / v <= 2^-24 (3 max(1, v - 1) / v + 1):
-// at most 1.9e-5 at v = 0.01 and below 2.4e-7 for v >= 1.  An error e in v
-// moves rhs = q + d - d v^3 + d ln v^3 by 3 e (d v^3 + d), and the test's band
-// 1e-5 (1 + |lu| + q + d + d v^3 + |d ln v^3|) covers that with room (at
-// v = 0.01: 5.7e-5 d against at least 1.4e-4 d; for v >= 1, 7e-7 (d v^3 + d)
-// against 1e-5 (d v^3 + d)), so a decided result is the exact fp64 decision.
-// +1 accept, 0 reject, -1 undecided (the caller takes the exact path).
-DEVI int mt_log_test_vf(float xf, float luf, float df, float vf) {
-  const float v3f = vf * vf * vf;
-  const float q = 0.5f * xf * xf, dv = df * v3f, dl = df * (3.0f * __builtin_amdgcn_logf(vf) * 0.693147180559945309f);
-  const float rhs = ((q + df) - dv) + dl;
-  const float tol = 1e-5f * (1.0f + fabsf(luf) + q + fabsf(df) + fabsf(dv) + fabsf(dl));
-  if (luf < rhs - tol) return 1;
-  if (luf > rhs + tol) return 0;
-  return -1;
 }
 
 // One Marsaglia-Tsang attempt from a (wave-uniform) table entry (x, log u,
@@ -512,46 +525,6 @@ DEVI f2v f_bar2(float x, float y, f2v xo, f2v yo) {
 
 constexpr int kRcWaves = 4;
 
-// attempt 0 of one gamma stream at (row, step), staged in LDS: x and log u in
-// fp32 (the common path's operands), +-log w in fp64 (the boost log-uniform)
-struct Tab0 {
-  float xf, luf;
-  double lw;
-};
-
-// One gamma by the fp32 common path: attempt 0 from LDS, attempts 1.. from
-// the table in global memory (wave-uniform entries).  false: an attempt the
-// fp32 tests cannot decide, or all tabulated attempts rejected -- the caller
-// takes the exact path (gamma_exact).
-DEVI bool gamma_fast(float c, float l2d, float df, const Tab0& e0, const double* tab, size_t plane, float& lg,
-                     double& lub) {
-  float xf = e0.xf, luf = e0.luf;
-  double lw = e0.lw;
-  for (int a = 0;;) {
-    const float vf = 1.0f + c * xf;
-    int dec;  // 1 accept, 0 reject, -1 undecided
-    if (!(fabsf(vf) > 1e-5f)) {
-      dec = -1;  // also NaN c (control 0)
-    } else if (!(vf > 0.0f)) {
-      dec = 0;
-    } else if (lw < 0.0) {
-      dec = 1;  // the squeeze accepted
-    } else {
-      dec = vf >= 0.01f ? mt_log_test_vf(xf, luf, df, vf) : -1;
-    }
-    if (dec == 1) {
-      lg = l2d + 3.0f * __builtin_amdgcn_logf(vf);
-      lub = -fabs(lw);
-      return true;
-    }
-    if (dec < 0 || ++a == kGammaTabAttempts) return false;
-    const double* e = tab + size_t(a) * 4 * plane;
-    xf = float(e[0]);
-    luf = float(e[2 * plane]);
-    lw = e[3 * plane];
-  }
-}
-
 // Fused baseline rollouts (see above): per step the four gammas by the fp32
 // common path (gamma_fast; attempt 0 staged in LDS), a gamma it cannot
 // decide by the exact path (gamma_exact), the Beta draws, then the rollout
@@ -579,7 +552,7 @@ __global__ __launch_bounds__(64 * kRcWaves) void k_roll_cand(Params p, int t) {
     for (int i = threadIdx.x; i < kRcWaves * H * 4; i += blockDim.x) {  // (row, step, stream), stream fastest
       const int k = i & 3, wh = i >> 2, rw = wh / H, h = wh - rw * H;
       const double* e = cf.gtab + k * sl + size_t(h) * S + r0 + min(rw, nr - 1);
-      t0[i] = Tab0{float(e[0]), float(e[2 * plane]), e[3 * plane]};
+      t0[i] = tab0_of(e, plane);
     }
   }
   __syncthreads();
@@ -625,12 +598,12 @@ __global__ __launch_bounds__(64 * kRcWaves) void k_roll_cand(Params p, int t) {
       st = m.ctl.y;
       const double* e = gt + size_t(h) * S;
       const float cv[4] = {m.c.x, m.c.y, m.c.z, m.c.w}, lv[4] = {m.l2d.x, m.l2d.y, m.l2d.z, m.l2d.w};
-      const float dv[4] = {m.d.x, m.d.y, m.d.z, m.d.w};
+      const float dv[4] = {m.d.x, m.d.y, m.d.z, m.d.w}, clv[4] = {m.clo.x, m.clo.y, m.clo.z, m.clo.w};
       float lg[4];
       double ug[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {  // the fp32 common path, else the exact path
-        if (!gamma_fast(cv[k], lv[k], dv[k], tw[h * 4 + k], e + k * sl, plane, lg[k], ug[k])) {
+        if (!gamma_fast(cv[k], clv[k], lv[k], dv[k], tw[h * 4 + k], e + k * sl, plane, lg[k], ug[k])) {
           const double alpha = double(((k & 1) ? 5.0f : 2.0f) * fabsf(k < 2 ? a : st));
           const uint32_t stream = k == 0 ? kStreamGammaAccA : k == 1 ? kStreamGammaAccB : k == 2 ? kStreamGammaSteerA
                                                                                                  : kStreamGammaSteerB;
