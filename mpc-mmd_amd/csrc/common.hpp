@@ -55,6 +55,66 @@ DEVI double readlane_d(double v, int l) {
   return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
 }
 
+// v_permlane32_swap (W = 32): lanes 32-63 of x <-> lanes 0-31 of y;
+// v_permlane16_swap (W = 16): the odd 16-lane rows of x <-> the even rows of y.
+// Inline asm: hipcc (ROCm 7.2) may commute the builtins' two operands, which
+// exchanges the other halves.  s_nop 1: the VALU-write -> permlane hazard.
+template <int W>
+DEVI void permlane_swap(float& x, float& y) {
+  if constexpr (W == 32)
+    __asm__ volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+  else
+    __asm__ volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+
+template <int W>
+DEVI void permlane_swap(double& x, double& y) {
+  const long long bx = __double_as_longlong(x), by = __double_as_longlong(y);
+  float xl = __int_as_float(int(bx)), xh = __int_as_float(int(bx >> 32));
+  float yl = __int_as_float(int(by)), yh = __int_as_float(int(by >> 32));
+  permlane_swap<W>(xl, yl);
+  permlane_swap<W>(xh, yh);
+  x = __longlong_as_double((static_cast<long long>(__float_as_int(xh)) << 32) | static_cast<unsigned>(__float_as_int(xl)));
+  y = __longlong_as_double((static_cast<long long>(__float_as_int(yh)) << 32) | static_cast<unsigned>(__float_as_int(yl)));
+}
+
+// wave totals of up to 16 per-lane fp64 values (v[n..15] taken as 0): lane l
+// ends with the total of v[l >> 2].  Each butterfly step halves the values a
+// lane carries (permlane32 / permlane16 swaps, then row_mirror and
+// row_half_mirror DPP keeping the half the pairing's lane bit selects, then
+// the quad) -- about a third of the instructions of n separate wave_sum trees.
+template <int n>
+DEVI double wave_totals16_d(const double (&v)[n]) {
+  static_assert(n <= 16, "at most 16 values");
+  const int lane = threadIdx.x & 63;
+  auto at = [&](int i) { return i < n ? v[i] : 0.0; };
+  double w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {  // lanes < 32 keep values 0..7, lanes >= 32 values 8..15
+    double a = at(i), b = at(i + 8);
+    permlane_swap<32>(a, b);
+    w[i] = a + b;
+  }
+  double x[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // odd rows keep the upper four
+    double a = w[i], b = w[i + 4];
+    permlane_swap<16>(a, b);
+    x[i] = a + b;
+  }
+  const bool b3 = lane & 8, b2 = lane & 4;
+  double y[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // row_mirror pairs l with l ^ 15 (bit 3 flipped)
+    const double keep = b3 ? x[i + 2] : x[i], send = b3 ? x[i] : x[i + 2];
+    y[i] = keep + dpp_d<0x140>(send);
+  }
+  // row_half_mirror pairs l with l ^ 7 (bit 2 flipped)
+  double z = (b2 ? y[1] : y[0]) + dpp_d<0x141>(b2 ? y[0] : y[1]);
+  z += dpp_d<0xB1>(z);
+  return z + dpp_d<0x4E>(z);
+}
+
 // ---- wave-wide reductions (wave-uniform result) --------------------------------
 // Sums: quad and row butterflies by DPP, then the row broadcasts into lane 63
 // and one readlane -- VALU only (a __shfl_xor butterfly is six LDS-crossbar

@@ -63,18 +63,6 @@ DEVI void wave_sync() {
   __asm__ volatile("" ::: "memory");
 }
 
-// v_permlane32_swap (W = 32): lanes 32-63 of x <-> lanes 0-31 of y;
-// v_permlane16_swap (W = 16): the odd 16-lane rows of x <-> the even rows of y.
-// Inline asm: hipcc (ROCm 7.2) may commute the builtins' two operands, which
-// exchanges the other halves.  s_nop 1: the VALU-write -> permlane hazard.
-template <int W>
-DEVI void permlane_swap(float& x, float& y) {
-  if constexpr (W == 32)
-    __asm__ volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
-  else
-    __asm__ volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
-}
-
 // sum over each row of 16 lanes (every lane of the row holds it)
 DEVI double row16_sum(double v) {
   v += dpp_d<0xB1>(v);

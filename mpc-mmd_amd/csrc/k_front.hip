@@ -38,14 +38,22 @@ DEVI float eval_row(const float (&r)[kNv], const double (&c)[kNv]) {
   return float(s);
 }
 
+// the 11 wave totals of s (fp64), rounded to fp32, in every lane
+DEVI void totals11(const double (&s)[kNv], float (&out)[kNv]) {
+  const double z = wave_totals16_d(s);
+#pragma unroll
+  for (int k = 0; k < kNv; ++k) out[k] = float(readlane_d(z, 4 * k));
+}
+
 // out[k] = fp32( sum_t M[t][k] r[t] ) over the wave's 100 points
 DEVI void adj(const float (&M0)[kNv], float r0, const float (&M1)[kNv], float r1, bool v1, float (&out)[kNv]) {
+  double s[kNv];
 #pragma unroll
   for (int k = 0; k < kNv; ++k) {
-    double s = double(M0[k]) * double(r0);
-    if (v1) s += double(M1[k]) * double(r1);
-    out[k] = float(wave_sum(s));
+    s[k] = double(M0[k]) * double(r0);
+    if (v1) s[k] += double(M1[k]) * double(r1);
   }
+  totals11(s, out);
 }
 
 // jnp.remainder(x, 2pi) for the unwrap (fmod, then shift into [0, 2pi))
@@ -70,17 +78,23 @@ DEVI void unwrap2(float& a0, float& a1, int lane, bool v1) {
   const float prev1 = lane == 0 ? last0 : up1;
   const float ph0 = lane == 0 ? 0.0f : unwrap_corr(a0 - prev0);
   const float ph1 = v1 ? unwrap_corr(a1 - prev1) : 0.0f;
-  // sequential cumsum (numpy / oracle order)
+  // sequential cumsum (numpy / oracle order) over the nonzero corrections only:
+  // adding a +0 leaves the fp32 running sum unchanged, so the sums are those of
+  // the full sequential scan; usually no correction is nonzero and nothing runs
   float acc = 0.0f, cs0 = 0.0f, cs1 = 0.0f;
-#pragma unroll
-  for (int i = 1; i < 64; ++i) {
+  unsigned long long m0 = __ballot(ph0 != 0.0f), m1 = __ballot(ph1 != 0.0f);
+  while (m0) {
+    const int i = __builtin_ctzll(m0);
+    m0 &= m0 - 1;
     acc = acc + readlane_f(ph0, i);
-    cs0 = lane == i ? acc : cs0;
+    cs0 = lane >= i ? acc : cs0;
   }
-#pragma unroll
-  for (int i = 0; i < kN - 64; ++i) {
+  cs1 = acc;
+  while (m1) {
+    const int i = __builtin_ctzll(m1);
+    m1 &= m1 - 1;
     acc = acc + readlane_f(ph1, i);
-    cs1 = lane == i ? acc : cs1;
+    cs1 = lane >= i ? acc : cs1;
   }
   if (lane > 0) a0 = a0 + cs0;
   if (v1) a1 = a1 + cs1;
@@ -122,6 +136,7 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
     }
   }
   __syncthreads();
+  MPCMMD_STAMP(p, 40);
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= p.Bt) return;
@@ -174,8 +189,10 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
   }
   float av0 = cr_atan2(yd[0], xd[0]), av1 = cr_atan2(yd[1], xd[1]);
   float aa0 = cr_atan2(ydd[0], xdd[0]), aa1 = cr_atan2(ydd[1], xdd[1]);
+  MPCMMD_STAMP(p, 41);
   unwrap2(av0, av1, lane, v1);
   unwrap2(aa0, aa1, lane, v1);
+  MPCMMD_STAMP(p, 42);
   Polar pv[2] = {polar_of(av0, xd[0], yd[0], 0.1f, 30.0f), polar_of(av1, xd[1], yd[1], 0.1f, 30.0f)};
   Polar pa[2] = {polar_of(aa0, xdd[0], ydd[0], 0.0f, 18.0f), polar_of(aa1, xdd[1], ydd[1], 0.0f, 18.0f)};
 
@@ -204,6 +221,7 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
     for (int k = 0; k < kNv; ++k) ly[k] = (ly[k] - tmp[k]) - tmp2[k];
   }
 
+  MPCMMD_STAMP(p, 43);
   // ---- compute_x (projection.py:123-185) --------------------------------------
   // lane-bound rows j = t-1 (t = 1..99): ub row j, lb row 99 + j; A_lane = [P[1:]; -P[1:]]
   const float y_ub = p.y_ub, mlb = -p.y_lb;  // b_lane: ub rows y_ub, lb rows -y_lb (gamma = 1)
@@ -238,13 +256,17 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
 #pragma unroll
     for (int k = 0; k < kNv; ++k) liny[k] = ((-ly[k] - fcyb[k]) - tmp[k]) - tmp2[k];
     // A_lane^T b_aug: sum_j P[j+1][k] (baug_ub[j] - baug_lb[j]) in fp64
+    double sa[kNv];
 #pragma unroll
     for (int k = 0; k < kNv; ++k) {
       double s = 0.0;
       if (h0) s += double(R.P[0][k]) * double(baug_ub[0]) - double(R.P[0][k]) * double(baug_lb[0]);
       if (v1) s += double(R.P[1][k]) * double(baug_ub[1]) - double(R.P[1][k]) * double(baug_lb[1]);
-      liny[k] = liny[k] - float(wave_sum(s));
+      sa[k] = s;
     }
+    totals11(sa, tmp);
+#pragma unroll
+    for (int k = 0; k < kNv; ++k) liny[k] = liny[k] - tmp[k];
     // KKT solve: c = Kinv[:11,:11] (-lincost) + Kinv[:11,11:] b_eq
 #pragma unroll
     for (int k = 0; k < kNv; ++k) {
@@ -290,6 +312,7 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
     sl[kN - 1 + j] = s_lb;
   }
 
+  MPCMMD_STAMP(p, 44);
   // ---- compute_alph_d (projection.py:193-274), no unwrap (Q13) ---------------
   Polar qv[2], qa[2];
   float alv[2], ala[2];
@@ -315,9 +338,13 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
       n_lane += double(rl_ub[q]) * double(rl_ub[q]) + double(rl_lb[q]) * double(rl_lb[q]);
     }
   }
-  n_acc = wave_sum(n_acc);
-  n_vel = wave_sum(n_vel);
-  n_lane = wave_sum(n_lane);
+  {
+    const double nv[3] = {n_acc, n_vel, n_lane};
+    const double z = wave_totals16_d(nv);
+    n_acc = readlane_d(z, 0);
+    n_vel = readlane_d(z, 4);
+    n_lane = readlane_d(z, 8);
+  }
   const float rn = (float(sqrt(n_acc)) + float(sqrt(n_vel))) + float(sqrt(n_lane));
   adj(R.DD[0], rax[0], R.DD[1], rax[1], v1, tmp);
   adj(R.D[0], rvx[0], R.D[1], rvx[1], v1, tmp2);
@@ -325,14 +352,22 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
   for (int k = 0; k < kNv; ++k) lx[k] = (lx[k] - tmp[k]) - tmp2[k];
   adj(R.DD[0], ray[0], R.DD[1], ray[1], v1, tmp);
   adj(R.D[0], rvy[0], R.D[1], rvy[1], v1, tmp2);
+  {
+    double sa[kNv];
+    float t3[kNv];
 #pragma unroll
-  for (int k = 0; k < kNv; ++k) {
-    double s = 0.0;
-    if (h0) s += double(R.P[0][k]) * double(rl_ub[0]) - double(R.P[0][k]) * double(rl_lb[0]);
-    if (v1) s += double(R.P[1][k]) * double(rl_ub[1]) - double(R.P[1][k]) * double(rl_lb[1]);
-    ly[k] = ((ly[k] - tmp[k]) - tmp2[k]) - float(wave_sum(s));
+    for (int k = 0; k < kNv; ++k) {
+      double s = 0.0;
+      if (h0) s += double(R.P[0][k]) * double(rl_ub[0]) - double(R.P[0][k]) * double(rl_lb[0]);
+      if (v1) s += double(R.P[1][k]) * double(rl_ub[1]) - double(R.P[1][k]) * double(rl_lb[1]);
+      sa[k] = s;
+    }
+    totals11(sa, t3);
+#pragma unroll
+    for (int k = 0; k < kNv; ++k) ly[k] = ((ly[k] - tmp[k]) - tmp2[k]) - t3[k];
   }
 
+  MPCMMD_STAMP(p, 45);
   // ---- compute_controls (cem_helper.py:540-551) ------------------------------
   float v[2], accv[2], steer[2];
 #pragma unroll
@@ -407,6 +442,7 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
     p.lam_y[size_t(b) * kNv + lane] = vly;
   }
   if (lane == 0) p.res_norm[b] = rn;
+  MPCMMD_STAMP(p, 46);
 }
 
 }  // namespace

@@ -45,6 +45,7 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
   while (N < B) N <<= 1;
   const int tid = threadIdx.x;
 
+  MPCMMD_STAMP(p, 32);
   // ---- argsort(res_norm), stable ------------------------------------------
   for (int i = tid; i < N; i += blockDim.x)
     keys[i] = i < B ? ((unsigned long long)sort_key(p.res_norm[g0 + i]) << 32) | unsigned(i) : ~0ull;
@@ -55,6 +56,7 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
     cf.tr_proj[size_t(t) * B + i] = perm[i];
   }
   __syncthreads();
+  MPCMMD_STAMP(p, 33);
   // ---- argsort(obs cost) over the permuted batch -------------------------
   for (int i = tid; i < N; i += blockDim.x)
     keys[i] = i < B ? ((unsigned long long)sort_key(p.obs_cost[g0 + perm[i]]) << 32) | unsigned(i) : ~0ull;
@@ -67,6 +69,7 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
   }
   __syncthreads();
 
+  MPCMMD_STAMP(p, 34);
   // ---- compute_cost of the 20 elites: one wave each ----------------------
   const int lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
   for (int j = w; j < kEliteCost; j += nw) {
@@ -154,6 +157,7 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
     }
   }
   __syncthreads();
+  MPCMMD_STAMP(p, 35);
   // ---- top 5 by cost (stable) -------------------------------------------
   if (tid < kEliteCost) {
     const uint32_t kj = sort_key(cost20[tid]);
@@ -229,6 +233,7 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
     for (int q = 0; q < kElite; ++q) cf.tr_cem[size_t(t) * kElite + q] = cem5[q];
   }
   __syncthreads();
+  MPCMMD_STAMP(p, 36);
   // ---- new population: [elites; mean + L z], v columns clipped -----------
   const float* z = cf.resample + size_t(t) * (B - kElite) * 8;
   for (int i = tid; i < B; i += blockDim.x) {
@@ -246,6 +251,7 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
     }
     for (int c = 0; c < 8; ++c) pop_next[size_t(i) * 8 + c] = row[c];
   }
+  MPCMMD_STAMP(p, 37);
   // ---- per-iteration result (cem.py:314-315) ------------------------------
   if (p.carla && tid < kN)  // steering of the chosen elite (carla/optimizer/cem.py:398-399, 419)
     p.res_steer[(size_t(cf.g) * p.T + t) * kN + tid] = p.steer[size_t(g0 + el[imin_s]) * kN + tid];

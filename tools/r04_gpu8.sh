@@ -1,0 +1,13 @@
+# k_front / k_select stamps, baseline parity, cvar timing (GPU box)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+timeout -k 10 200 python tools/stamps_cvar.py cvar > gpurun_out/st.log 2>&1 && \
+timeout -k 10 200 python tools/stamps_cvar.py mmd_opt >> gpurun_out/st.log 2>&1 && cat gpurun_out/st.log || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity_baseline.py tests/test_gpu_free_run.py ${EXTRA_TESTS} -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu > gpurun_out/t.log 2>&1; rc=$?; tail -3 gpurun_out/t.log; [ $rc -eq 0 ] || exit 1
+for wl in ${WORKLOADS:-cvar}; do
+  timeout -k 10 200 python bench.py --workload $wl --steps 100 --warmup 10 --cpu-seconds 0 --extra 0 > gpurun_out/ab_$wl.json || exit 1
+  python -c "
+import json
+d=json.load(open('gpurun_out/ab_$wl.json')); print('$wl', round(d['value'],1), {k:round(v*1e3,1) for k,v in d['kernels_ms_per_step'].items()})"
+done
