@@ -100,6 +100,70 @@ DEVI unsigned long long max8_u64(unsigned long long v) {
   return step(v, [](int x) { return dpp_i<0x141>(x); });
 }
 
+// smallest 64-bit word over each group of 8 lanes, in every lane of the group
+DEVI unsigned long long min8_u64(unsigned long long v) {
+  auto step = [](unsigned long long a, auto dpp) {
+    const unsigned long long b = (static_cast<unsigned long long>(unsigned(dpp(int(a >> 32)))) << 32) |
+                                 unsigned(dpp(int(a)));
+    return b < a ? b : a;
+  };
+  v = step(v, [](int x) { return dpp_i<0xB1>(x); });
+  v = step(v, [](int x) { return dpp_i<0x4E>(x); });
+  return step(v, [](int x) { return dpp_i<0x141>(x); });
+}
+
+// The K smallest of B <= blockDim.x distinct 64-bit words (one per thread,
+// w = ~0 for threads >= B), in ascending order: out(rank, w) for rank < K.
+// Window as in block_cvar: T0 = the K-th smallest of the 8-lane group minima
+// (the K groups whose minimum is <= T0 hold K words <= T0, so every one of
+// the K smallest is <= T0, and at most K groups contribute), the words <= T0
+// compacted into LDS and ranked exactly among themselves.  gm: B / 8 + 2
+// words, list: 8 K + 2 words (16-byte aligned), cnt / t0: LDS scalars.
+template <class Out>
+DEVI void block_smallest(unsigned long long w, int B, int K, unsigned long long* gm, unsigned long long* list,
+                         int& cnt, unsigned long long& t0, Out out) {
+  const int tid = threadIdx.x, G = (B + 7) >> 3;
+  const unsigned long long m = min8_u64(w);
+  if ((tid & 7) == 0 && tid < 8 * G) gm[tid >> 3] = m;
+  if (tid == 0) {
+    cnt = 0;
+    t0 = ~0ull;  // fewer than K groups: every word is in the window
+  }
+  __syncthreads();
+  if (tid == 0) gm[G] = ~0ull;  // pads the pair reads (never smaller)
+  __syncthreads();
+  if (G > K && tid < G) {
+    const unsigned long long mg = gm[tid];  // group tid's minimum
+    const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(gm);
+    int r = 0;
+#pragma unroll 8
+    for (int q = 0; q < (G + 1) >> 1; ++q) {  // LDS broadcast reads, several in flight
+      const ulonglong2 v = g2[q];
+      r += int(v.x < mg) + int(v.y < mg);
+    }
+    if (r == K - 1) t0 = mg;
+  }
+  __syncthreads();
+  const unsigned long long T0 = t0;
+  if (tid < B && w <= T0) list[atomicAdd(&cnt, 1)] = w;
+  __syncthreads();
+  const int c = cnt;
+  if (tid == 0) list[c] = ~0ull;
+  __syncthreads();
+  const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(list);
+  for (int a = tid; a < c; a += blockDim.x) {
+    const unsigned long long ka = list[a];
+    int r = 0;
+#pragma unroll 8
+    for (int q = 0; q < (c + 1) >> 1; ++q) {
+      const ulonglong2 v = l2[q];
+      r += int(v.x < ka) + int(v.y < ka);
+    }
+    if (r < K) out(r, ka);
+  }
+  __syncthreads();
+}
+
 // jnp.quantile(x, 0.98) (linear, JAX fp32 weights) + mean of the tail
 // (costs.py:215-219) over vals[0..S).  list: >= S 64-bit words of LDS.
 // Sorted order = the jnp.argsort total order (ties by index): the words

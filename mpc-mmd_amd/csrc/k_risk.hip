@@ -28,6 +28,8 @@ namespace {
 struct RiskLds {
   float* xo;
   float* yo;
+  float* xs;  // [H][O] obstacles of each step sorted by x (k_risk_baseline's window)
+  float* ys;
   float* a;
   float* st;
   float* cbar;
@@ -43,6 +45,10 @@ DEVI RiskLds carve(char* base, int O, int H, int S) {
   L.xo = f;
   f += O * H;
   L.yo = f;
+  f += O * H;
+  L.xs = f;
+  f += O * H;
+  L.ys = f;
   f += O * H;
   L.a = f;
   f += H;
@@ -66,7 +72,7 @@ DEVI RiskLds carve(char* base, int O, int H, int S) {
 }  // namespace
 
 size_t risk_lds_bytes(int O, int H, int S) {
-  size_t f = size_t(2 * O * H + 2 * H + 3 * S) * 4;
+  size_t f = size_t(4 * O * H + 2 * H + 3 * S) * 4;
   f = (f + 15) & ~size_t(15);
   f += size_t(S) * 8;  // (key, index) pairs of block_cvar
   f = (f + 15) & ~size_t(15);
@@ -90,6 +96,27 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
     L.st[h] = p.steer[size_t(b) * 100 + h];
   }
   __syncthreads();
+  // each step's obstacles sorted by x (insertion sort, a thread per step);
+  // a NaN obstacle coordinate keeps the full scan for the whole candidate
+  constexpr int kWindowMaxObs = 64;  // above: the full scan (the sort is O^2 per step)
+  bool any_nan = O > kWindowMaxObs;
+  for (int h = threadIdx.x; h < H && O <= kWindowMaxObs; h += blockDim.x) {
+    float* xs = L.xs + h * O;
+    float* ys = L.ys + h * O;
+    for (int o = 0; o < O; ++o) {
+      const float xv = L.xo[o * H + h], yv = L.yo[o * H + h];
+      any_nan |= (xv != xv) | (yv != yv);
+      int k = o;
+      while (k > 0 && xs[k - 1] > xv) {
+        xs[k] = xs[k - 1];
+        ys[k] = ys[k - 1];
+        --k;
+      }
+      xs[k] = xv;
+      ys[k] = yv;
+    }
+  }
+  const bool window = !__syncthreads_or(any_nan);
   const float* bpl = p.noise == 1 ? p.bplane + size_t(b) * 2 * H * S : nullptr;
   const size_t HS = size_t(H) * S;
   for (int r = threadIdx.x; r < S; r += blockDim.x) {
@@ -104,14 +131,36 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
     float c0 = n01[0], c1 = n01[HS], c2 = rl[2 * HS];
     for (int h = 0; h < H; ++h) {
       // residual of the recorded state (x_roll[:, h] = state before step h)
-      for (int o = 0; o < O; ++o) {
-        // |x - x_o| >= a gives (x - x_o)^2 / a^2 >= 1 (monotone roundings), so
-        // f_bar <= 0 cannot raise the maximum: skipped (whole waves, as a rule)
-        const float xo = L.xo[o * H + h];
-        if (!(fabsf(x - xo) >= kObsA)) {
-          const float c = f_bar(x, y, xo, L.yo[o * H + h]);
+      // |x - x_o| >= a gives (x - x_o)^2 / a^2 >= 1 (monotone roundings), so
+      // f_bar <= 0 cannot raise the maximum: skipped.  With the step's
+      // obstacles sorted by x, fl(x - x_o) falls as x_o grows, so the ones
+      // left are a contiguous run: its start by binary search, then the run
+      if (window) {
+        const float* xs = L.xs + h * O;
+        const float* ys = L.ys + h * O;
+        int lo = 0, hi = O;  // first o with x - xs[o] < a
+        for (int it = 0; (1 << it) <= O; ++it) {  // ceil(log2(O + 1)) halvings
+          const int mid = (lo + hi) >> 1;
+          const bool go = lo < hi && !(x - xs[min(mid, O - 1)] < kObsA);
+          const bool left = lo < hi && !go;
+          lo = go ? mid + 1 : lo;
+          hi = left ? mid : hi;
+        }
+        for (int o = lo; o < O; ++o) {
+          const float xo = xs[o];
+          if (fabsf(x - xo) >= kObsA) break;
+          const float c = f_bar(x, y, xo, ys[o]);
           nan |= (c != c);
           cb = fmaxf(cb, c);
+        }
+      } else {
+        for (int o = 0; o < O; ++o) {
+          const float xo = L.xo[o * H + h];
+          if (!(fabsf(x - xo) >= kObsA)) {
+            const float c = f_bar(x, y, xo, L.yo[o * H + h]);
+            nan |= (c != c);
+            cb = fmaxf(cb, c);
+          }
         }
       }
       const float l1 = -y + p.y_lb, u1 = y - p.y_ub;
@@ -696,8 +745,10 @@ void launch_beta_planes(const Params& p, int t, hipStream_t s) {
                        t);
   } else {
     const int groups = (p.B + 63) / 64;
-    hipLaunchKernelGGL(k_beta_planes_c, dim3((p.S + kBpRows - 1) / kBpRows, p.H, p.G * groups), dim3(256), 0, s, p,
-                       t);
+    // the last step's draws move nothing (k_risk_baseline never applies them):
+    // not drawn, except for the parity tests' plane dump
+    hipLaunchKernelGGL(k_beta_planes_c, dim3((p.S + kBpRows - 1) / kBpRows, p.beta_dump ? p.H : p.H - 1, p.G * groups),
+                       dim3(256), 0, s, p, t);
   }
   hipLaunchKernelGGL(k_beta_fix, dim3(256), dim3(256), 0, s, p, t);
 }

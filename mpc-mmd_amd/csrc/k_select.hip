@@ -28,7 +28,7 @@ constexpr int kMaxSortN = 4096;
 constexpr int kN = 100;
 
 __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
-  __shared__ unsigned long long keys[kMaxSortN];
+  __shared__ __attribute__((aligned(16))) unsigned long long keys[kMaxSortN];
   __shared__ int perm[kMaxSortN];
   __shared__ int el[kEliteCost];
   __shared__ float cost20[kEliteCost];
@@ -58,17 +58,28 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
   __syncthreads();
   MPCMMD_STAMP(p, 33);
   // ---- argsort(obs cost) over the permuted batch -------------------------
-  for (int i = tid; i < N; i += blockDim.x)
-    keys[i] = i < B ? ((unsigned long long)sort_key(p.obs_cost[g0 + perm[i]]) << 32) | unsigned(i) : ~0ull;
-  if (N <= int(blockDim.x)) bitonic_sort_reg(keys, N);
-  else bitonic_sort(keys, N);
-  if (tid < kEliteCost) {
-    const int e = perm[int(keys[tid] & 0xFFFFFFFFu)];
-    el[tid] = e;  // candidate index within the configuration
-    cf.tr_obs[size_t(t) * kEliteCost + tid] = e;
+  if (B <= int(blockDim.x) && B >= kEliteCost) {  // only the 20 smallest words are needed: a window selection
+    __shared__ int wcnt;
+    __shared__ unsigned long long wt0;
+    const unsigned long long wv =
+        tid < B ? ((unsigned long long)sort_key(p.obs_cost[g0 + perm[tid]]) << 32) | unsigned(tid) : ~0ull;
+    block_smallest(wv, B, kEliteCost, keys, keys + 1024, wcnt, wt0, [&](int r, unsigned long long k) {
+      const int e = perm[int(k & 0xFFFFFFFFu)];
+      el[r] = e;  // candidate index within the configuration
+      cf.tr_obs[size_t(t) * kEliteCost + r] = e;
+    });
+  } else {
+    for (int i = tid; i < N; i += blockDim.x)
+      keys[i] = i < B ? ((unsigned long long)sort_key(p.obs_cost[g0 + perm[i]]) << 32) | unsigned(i) : ~0ull;
+    if (N <= int(blockDim.x)) bitonic_sort_reg(keys, N);
+    else bitonic_sort(keys, N);
+    if (tid < kEliteCost) {
+      const int e = perm[int(keys[tid] & 0xFFFFFFFFu)];
+      el[tid] = e;  // candidate index within the configuration
+      cf.tr_obs[size_t(t) * kEliteCost + tid] = e;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-
   MPCMMD_STAMP(p, 34);
   // ---- compute_cost of the 20 elites: one wave each ----------------------
   const int lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
@@ -127,18 +138,20 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
       }
       if (tt < kN - 2) n_sa += double(sa[q]) * double(sa[q]);
     }
-    n_des = sqrt(wave_sum(n_des));
-    n_st = sqrt(wave_sum(n_st));
-    n_sv = sqrt(wave_sum(n_sv));
-    n_sa = sqrt(wave_sum(n_sa));
-    n_v = sqrt(wave_sum(n_v));
-    n_sp = sqrt(wave_sum(n_sp));
-    n_svp = sqrt(wave_sum(n_svp));
-    n_ydd = sqrt(wave_sum(n_ydd));
-    n_xdd = sqrt(wave_sum(n_xdd));
-    if (p.carla) {
-      n_des2 = sqrt(wave_sum(n_des2));
-      n_cen = sqrt(wave_sum(n_cen));
+    {  // the eleven wave totals at once (lanes 4 k .. 4 k + 3 hold total k)
+      const double nv[11] = {n_des, n_st, n_sv, n_sa, n_v, n_sp, n_svp, n_ydd, n_xdd, n_des2, n_cen};
+      const double z = wave_totals16_d(nv);
+      n_des = sqrt(readlane_d(z, 0));
+      n_st = sqrt(readlane_d(z, 4));
+      n_sv = sqrt(readlane_d(z, 8));
+      n_sa = sqrt(readlane_d(z, 12));
+      n_v = sqrt(readlane_d(z, 16));
+      n_sp = sqrt(readlane_d(z, 20));
+      n_svp = sqrt(readlane_d(z, 24));
+      n_ydd = sqrt(readlane_d(z, 28));
+      n_xdd = sqrt(readlane_d(z, 32));
+      n_des2 = sqrt(readlane_d(z, 36));
+      n_cen = sqrt(readlane_d(z, 40));
     }
     if (lane == 0) {
       const double cobs = double(p.w_obs * p.obs_cost[e]);
@@ -206,20 +219,27 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
     if (tid < 8) cf.mean[tid] = mean32[tid];
     wave_sync_lds();
   }
-  if (tid == 0) {
-    // Cholesky (lower) of the fp32 covariance, in fp64
+  if (tid < 64) {
+    // Cholesky (lower) of the fp32 covariance, in fp64: column j's pivot on
+    // lane j, then its entries below on lanes i > j in parallel (each entry's
+    // sum in the serial algorithm's order, so the same bits)
     for (int j = 0; j < 8; ++j) {
-      double d = cvs[j][j];
-      for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k];
-      d = sqrt(d);
-      L[j][j] = d;
-      for (int i = j + 1; i < 8; ++i) {
-        double s = cvs[i][j];
-        for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k];
-        L[i][j] = s / d;
+      if (tid == j) {
+        double d = cvs[j][j];
+        for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k];
+        L[j][j] = sqrt(d);
       }
-      for (int i = 0; i < j; ++i) L[i][j] = 0.0;
+      wave_sync_lds();
+      if (tid > j && tid < 8) {
+        double s = cvs[tid][j];
+        for (int k = 0; k < j; ++k) s -= L[tid][k] * L[j][k];
+        L[tid][j] = s / L[j][j];
+      }
+      if (tid < j) L[tid][j] = 0.0;
+      wave_sync_lds();
     }
+  }
+  if (tid == 0) {
     // idx_min = argmin(cost_batch_temp) (== 0 unless NaN; jnp.argmin: first NaN)
     int im = 0;
     for (int q = 0; q < kElite; ++q) {

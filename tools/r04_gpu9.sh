@@ -3,7 +3,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 timeout -k 10 200 python tools/stamps_cvar.py cvar > gpurun_out/st.log 2>&1 && cat gpurun_out/st.log || exit 1
-timeout -k 10 900 python -u -m pytest tests/test_gpu_parity_mmdopt.py tests/test_gpu_parity_baseline.py tests/test_gpu_free_run.py tests/test_gpu_full_shape.py tests/test_gpu_configs0.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu > gpurun_out/t.log 2>&1; rc=$?; tail -3 gpurun_out/t.log; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/t.log | head -20; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_parity_mmdopt.py tests/test_gpu_parity_baseline.py tests/test_gpu_free_run.py tests/test_gpu_full_shape.py tests/test_gpu_configs0.py tests/test_gpu_carla.py tests/test_validation_golden.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu > gpurun_out/t.log 2>&1; rc=$?; tail -3 gpurun_out/t.log; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/t.log | head -20; exit 1; }
 for wl in cvar mmd_opt; do
   timeout -k 10 300 python bench.py --workload $wl --steps 30 --warmup 5 --cpu-seconds 0 --extra 0 > gpurun_out/ab_$wl.json || exit 1
   python -c "
