@@ -297,7 +297,7 @@ def run_workload(name, steps, warmup, profile_steps, rank, world, local, dist=No
                               num_batch=w["num_batch"], maxiter_cem=T, device=local, seed=rank,
                               variant=w.get("variant", "static"))
     h = _native.Handle(cfg)
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()  # a created stream (the legacy default stream cannot be graph-captured)
     h.set_stream(stream.cuda_stream)
 
     def run(k0, count, evs=None):

@@ -117,7 +117,7 @@ struct mpcmmd_handle {
   // length, external draws, configurations) and replayed (one hipGraphLaunch
   // instead of ~150 launches per outer iteration)
   bool graphs = false;
-  std::map<std::tuple<int, int, int, int>, std::pair<hipGraph_t, hipGraphExec_t>> gexec;
+  std::map<std::tuple<int, int, int, int, int, int>, std::pair<hipGraph_t, hipGraphExec_t>> gexec;
   // profiling
   bool prof = false;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -979,8 +979,8 @@ int mpcmmd_iterate(mpcmmd_handle* h, int32_t t_begin, int32_t count) {
   if (t_begin < 0 || count < 0 || t_begin + count > h->T) return fail(MPCMMD_E_INVALID, "iteration range");
   return guarded([&] {
     check_device(h);
-    auto body = [&] {
-      for (int t = t_begin; t < t_begin + count; ++t) {
+    auto body = [&](int t_lo, int cnt) {
+      for (int t = t_lo; t < t_lo + cnt; ++t) {
         if (!h->ext_roll || !h->ext_res) {
           if (h->ext_roll != h->ext_res) throw std::invalid_argument("roll and resample draws go together");
           run_stage(h, 0, t);
@@ -990,18 +990,22 @@ int mpcmmd_iterate(mpcmmd_handle* h, int32_t t_begin, int32_t count) {
         run_stage(h, 3, t);
       }
     };
-    // a whole solve on one stream (the candidate groups of large batches
-    // fork onto other streams: launched directly)
-    const bool one_stream = h->p.Bt < 1024 && !h->groups_forced;
-    if (h->graphs && !h->prof && one_stream && t_begin == 0 && count == h->T) {
+    // graphs of a whole solve (count == T) or of single iterations (count ==
+    // 1: all T captured at the first use, so no capture lands in a timed
+    // loop) on one stream -- the beta-CEM candidate groups of large mmd_opt
+    // batches fork onto other streams and are launched directly
+    const bool one_stream = h->cost != MPCMMD_COST_MMD_OPT || (h->p.Bt < 1024 && !h->groups_forced);
+    const bool whole = t_begin == 0 && count == h->T;
+    if (h->graphs && !h->prof && one_stream && (whole || count == 1)) {
       if (h->cost == MPCMMD_COST_MMD_OPT) ensure_sel0(h);  // host read-back: never inside a capture
-      const auto key = std::make_tuple(h->cost, h->p.P, int(h->ext_roll), h->G);
-      auto it = h->gexec.find(key);
-      if (it == h->gexec.end()) {
+      auto key_of = [&](int tb, int cnt) {
+        return std::make_tuple(h->cost, h->p.P, int(h->ext_roll), h->G, whole ? 0 : tb, cnt);
+      };
+      auto capture = [&](int tb, int cnt) {
         hipGraph_t g = nullptr;
         HIPC(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
         try {
-          body();
+          body(tb, cnt);
         } catch (...) {
           (void)hipStreamEndCapture(h->stream, &g);
           if (g) (void)hipGraphDestroy(g);
@@ -1010,11 +1014,19 @@ int mpcmmd_iterate(mpcmmd_handle* h, int32_t t_begin, int32_t count) {
         HIPC(hipStreamEndCapture(h->stream, &g));
         hipGraphExec_t e = nullptr;
         HIPC(hipGraphInstantiate(&e, g, nullptr, nullptr, 0));
-        it = h->gexec.emplace(key, std::make_pair(g, e)).first;
+        h->gexec.emplace(key_of(tb, cnt), std::make_pair(g, e));
+      };
+      if (h->gexec.find(key_of(t_begin, count)) == h->gexec.end()) {
+        if (whole) {
+          capture(0, h->T);
+        } else {
+          for (int tb = 0; tb < h->T; ++tb)
+            if (h->gexec.find(key_of(tb, 1)) == h->gexec.end()) capture(tb, 1);
+        }
       }
-      HIPC(hipGraphLaunch(it->second.second, h->stream));
+      HIPC(hipGraphLaunch(h->gexec.find(key_of(t_begin, count))->second.second, h->stream));
     } else {
-      body();
+      body(t_begin, count);
     }
     h->last_t = t_begin + count - 1;
     return MPCMMD_OK;
