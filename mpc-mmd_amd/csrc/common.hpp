@@ -149,10 +149,21 @@ DEVI double wave_total(double v) {
 DEVI double wave_sum(double v) { return wave_total(v); }
 DEVI float wave_sum(float v) { return wave_total(v); }
 DEVI int wave_sum(int v) { return wave_total(v); }
+// wave maximum (fmaxf: NaN ignored unless every lane is NaN), VALU only: quad
+// and row butterflies, then the row broadcasts into lane 63 (rows a broadcast
+// does not write keep their own value: old = v), one readlane
+template <int CTRL, int ROWS = 0xF>
+DEVI float dpp_keep_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, ROWS, 0xF, false));
+}
 DEVI float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
-  return v;
+  v = fmaxf(v, dpp_keep_f<0xB1>(v));
+  v = fmaxf(v, dpp_keep_f<0x4E>(v));
+  v = fmaxf(v, dpp_keep_f<0x124>(v));
+  v = fmaxf(v, dpp_keep_f<0x128>(v));
+  v = fmaxf(v, dpp_keep_f<0x142, 0xA>(v));
+  v = fmaxf(v, dpp_keep_f<0x143, 0xC>(v));
+  return readlane_f(v, 63);
 }
 DEVI unsigned long long wave_max_u64(unsigned long long v) {
 #pragma unroll
