@@ -717,18 +717,34 @@ __global__ __launch_bounds__(512) void k_risk_reduce(Params p, int t) {
 }
 
 // the deferred elements of k_beta_planes, through the full sampler
+// a quad per element: lane k of the quad runs gamma k (acc a, acc b, steer a,
+// steer b) through the full sampler (gamma_parts_tab, as beta_pair), lanes 0
+// and 2 combine their pair (beta_combine): beta_pair's bits, a quarter of
+// its serial chain (the launch's time is one element's latency)
 __global__ __launch_bounds__(256) void k_beta_fix(Params p, int t) {
   const int S = p.S, H = p.H;
   const unsigned cnt = *p.bfix_n;
-  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
-    const uint32_t e = p.bfix[i];
+  const int lane = threadIdx.x & 63, k = lane & 3, q0 = lane & ~3;
+  const size_t sl = size_t(kGammaTabAttempts) * 4 * S * H;  // one stream's table
+  const uint32_t streams[4] = {kStreamGammaAccA, kStreamGammaAccB, kStreamGammaSteerA, kStreamGammaSteerB};
+  for (unsigned gi = blockIdx.x * blockDim.x + threadIdx.x; gi < 4 * cnt; gi += gridDim.x * blockDim.x) {
+    const uint32_t e = p.bfix[gi >> 2];
     const int r = int(e % uint32_t(S)), bh = int(e / uint32_t(S));
     const int h = bh % H, b = bh / H;
-    float nba, nbs;
-    beta_pair(p, cfg_of(p, b / p.B), t, r, h, p.acc[size_t(b) * 100 + h], p.steer[size_t(b) * 100 + h], nba, nbs);
-    float* o = p.bplane + size_t(b) * 2 * H * S;
-    o[size_t(h) * S + r] = nba;
-    o[(size_t(H) + h) * S + r] = nbs;
+    const Cfg cf = cfg_of(p, b / p.B);
+    const float fa = fabsf(p.acc[size_t(b) * 100 + h]), fs = fabsf(p.steer[size_t(b) * 100 + h]);
+    const double al[4] = {double(2.0f * fa), double(5.0f * fa), double(2.0f * fs), double(5.0f * fs)};
+    const double alpha = k == 0 ? al[0] : k == 1 ? al[1] : k == 2 ? al[2] : al[3];
+    const uint32_t stream = k == 0 ? streams[0] : k == 1 ? streams[1] : k == 2 ? streams[2] : streams[3];
+    double g, u;
+    gamma_parts_tab(mt_const(alpha), cf.gtab + size_t(k) * sl, S, H, r, h, iteration_key0(cf.idx_mpc, t), p.seed,
+                    stream, uint32_t(r) * uint32_t(H) + uint32_t(h), g, u);
+    const double g1 = __shfl(g, q0 + (k | 1), 64), u1 = __shfl(u, q0 + (k | 1), 64);  // the pair's b gamma
+    if ((k & 1) == 0) {
+      const double a = k == 0 ? al[0] : al[2], bb = k == 0 ? al[1] : al[3];
+      const float v = beta_combine(a, bb, 2.0, 5.0, g, u, g1, u1);
+      p.bplane[size_t(b) * 2 * H * S + (size_t(k == 0 ? 0 : H) + h) * S + r] = v;
+    }
   }
 }
 
@@ -750,7 +766,7 @@ void launch_beta_planes(const Params& p, int t, hipStream_t s) {
     hipLaunchKernelGGL(k_beta_planes_c, dim3((p.S + kBpRows - 1) / kBpRows, p.beta_dump ? p.H : p.H - 1, p.G * groups),
                        dim3(256), 0, s, p, t);
   }
-  hipLaunchKernelGGL(k_beta_fix, dim3(256), dim3(256), 0, s, p, t);
+  hipLaunchKernelGGL(k_beta_fix, dim3(1024), dim3(256), 0, s, p, t);
 }
 
 void launch_gamma_tab(const Params& p, int t, hipStream_t s) {
