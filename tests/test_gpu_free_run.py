@@ -121,3 +121,29 @@ def test_free_run(native, cost, noise, n):
             close("res_beta", got["res_beta"], ref[6], rtol=1e-4, atol=1e-6)
     print(f"{cost}/{noise}: 20 iterations in lockstep; cost_obs {float(got['cost_obs'])}; "
           f"explained beta-CEM partings {parted}; Beta-draw cost moves {moved}")
+
+
+@pytest.mark.parametrize("cost,noise,n", [("cvar", "beta", 24), ("mmd_opt", "gaussian", 6)])
+def test_iteration_graphs(native, cost, noise, n):
+    """Single-iteration graph replay (mpcmmd_set_graphs, then iterate(t, 1):
+    all T iterations captured at the first call) gives the bits of direct
+    launches, and again when the captured graphs are reused by a new solve."""
+    from parity import make_pair
+    Tg = 6
+    ora, nat, xo, yo = make_pair(native, cost, noise, n=n, O=O, H=10, B=B, T=Tg)
+
+    def run(graphs):
+        nat.set_graphs(graphs)
+        nat.begin(cost, 3, DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, xo, yo, 15.0)
+        for t in range(Tg):
+            nat.iterate(t, 1)
+        return nat.finish()
+
+    ref = run(False)
+    for rep in range(2):
+        got = run(True)
+        for k, v in ref.items():
+            if isinstance(v, np.ndarray):
+                assert np.array_equal(got[k], v, equal_nan=True), f"{k} differs with graphs (run {rep})"
+            else:
+                assert got[k] == v or (v != v and got[k] != got[k]), f"{k} differs with graphs (run {rep})"

@@ -192,3 +192,13 @@ def test_free_run_solve(native):
     assert float(ref[3]) == 0.0 and float(got["cost_obs"]) == 0.0
     close("cx[:3]", got["cx"][:3], ref[0][:3], atol=1e-4)
     close("cy[:3]", got["cy"][:3], ref[1][:3], atol=1e-4)
+
+
+@pytest.mark.parametrize("cost,noise", [("cvar", "beta"), ("saa", "gaussian")])
+def test_iteration_lockstep_fused_risk(native, monkeypatch, cost, noise):
+    """The opt-in fused risk path (MPCMMD_RISK_FUSED=1: Beta draws inside the
+    candidate-lane rollouts, k_risk_reduce) against the oracle, iteration by
+    iteration, like the default row-lane path."""
+    monkeypatch.setenv("MPCMMD_RISK_FUSED", "1")  # read when the handle is created
+    exact = run_iteration_lockstep(native, cost, noise)
+    assert exact >= 15, f"only {exact}/20 iterations had identical elite sets"
