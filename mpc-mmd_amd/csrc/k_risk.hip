@@ -129,6 +129,7 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
     const float* rl = cf.roll + size_t(t) * 3 * HS + r;
     const float* n01 = p.noise == 1 ? bpl + r : rl;  // [2][H][S] planes or roll rows 0, 1
     float c0 = n01[0], c1 = n01[HS], c2 = rl[2 * HS];
+    int lo_prev = 0;  // the obstacle window's start at the previous step
     for (int h = 0; h < H; ++h) {
       // residual of the recorded state (x_roll[:, h] = state before step h)
       // |x - x_o| >= a gives (x - x_o)^2 / a^2 >= 1 (monotone roundings), so
@@ -138,14 +139,13 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
       if (window) {
         const float* xs = L.xs + h * O;
         const float* ys = L.ys + h * O;
-        int lo = 0, hi = O;  // first o with x - xs[o] < a
-        for (int it = 0; (1 << it) <= O; ++it) {  // ceil(log2(O + 1)) halvings
-          const int mid = (lo + hi) >> 1;
-          const bool go = lo < hi && !(x - xs[min(mid, O - 1)] < kObsA);
-          const bool left = lo < hi && !go;
-          lo = go ? mid + 1 : lo;
-          hi = left ? mid : hi;
-        }
+        // lo = the first o with x - xs[o] < a (a monotone predicate), found
+        // by walking from the previous step's lo: the rollout and the
+        // obstacles move little per step, so usually no step is taken
+        int lo = lo_prev;
+        while (lo < O && !(x - xs[lo] < kObsA)) ++lo;
+        while (lo > 0 && x - xs[lo - 1] < kObsA) --lo;
+        lo_prev = lo;
         for (int o = lo; o < O; ++o) {
           const float xo = xs[o];
           if (fabsf(x - xo) >= kObsA) break;
