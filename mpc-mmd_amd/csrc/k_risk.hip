@@ -366,7 +366,8 @@ DEVI bool gamma_fast(float c, float clo, float l2d, float df, const Tab0& e0, co
   }
 }
 
-constexpr int kBpRows = 32;  // rows per k_beta_planes_c workgroup (8 per wave)
+constexpr int kBpRows = 32;   // rows per k_beta_planes_c chunk (8 per wave)
+constexpr int kBpChunks = 1;  // chunks per workgroup (more measured slower: 2 -> +10%, 4 -> +25%)
 
 // Beta(a, b) = 1 / (1 + 2^(log2 Gb - log2 Ga)) from the gammas' log2 G' and
 // boost log-uniforms (beta_combine's formula, the log2 G' given).
@@ -396,19 +397,14 @@ DEVI float beta_from_logs(double a, double b, double ra, double rb, float lga, d
 __global__ __launch_bounds__(256) void k_beta_planes_c(Params p, int t) {
   const int S = p.S, H = p.H;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r0 = blockIdx.x * kBpRows, h = blockIdx.y;
+  const int h = blockIdx.y;
   const int groups = (p.B + 63) / 64;
   const int g = blockIdx.z / groups, j0 = (blockIdx.z - g * groups) * 64;
-  const int nc = min(64, p.B - j0), nr = min(kBpRows, S - r0);
+  const int nc = min(64, p.B - j0);
   const double* gt = p.gtab + size_t(g) * gtab_stride(S, H);
   const size_t plane = size_t(S) * H, sl = size_t(kGammaTabAttempts) * 4 * plane;
   __shared__ Tab0 t0[4][kBpRows];
   __shared__ float tile[2][kBpRows][65];
-  for (int q = threadIdx.x; q < 4 * kBpRows; q += blockDim.x) {  // attempt 0, streams acc A/B, steer A/B
-    const int k = q / kBpRows, rl = q - k * kBpRows;
-    const double* e = gt + k * sl + size_t(h) * S + r0 + min(rl, nr - 1);
-    t0[k][rl] = tab0_of(e, plane);
-  }
   const int c = min(lane, nc - 1);
   const uint32_t b = uint32_t(g) * p.B + j0 + c;
   const float fa = fabsf(p.acc[size_t(b) * 100 + h]), fs = fabsf(p.steer[size_t(b) * 100 + h]);
@@ -416,37 +412,49 @@ __global__ __launch_bounds__(256) void k_beta_planes_c(Params p, int t) {
   const double al[4] = {aa, ab, sa, sb};
   float cv[4], cl[4], lv[4], dv[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {  // the gammas' constants (k_mt_tab's)
+  for (int k = 0; k < 4; ++k) {  // the gammas' constants (k_mt_tab's), once for the workgroup's chunks
     const MtConst m = mt_const(al[k]);
     cv[k] = float(m.c);
     cl[k] = float(m.c - double(cv[k]));
     lv[k] = __builtin_amdgcn_logf(float(m.d));
     dv[k] = float(m.d);
   }
-  __syncthreads();
-  for (int i = 0; i < kBpRows / 4; ++i) {
-    const int rl = w * (kBpRows / 4) + i, r = r0 + rl;
-    if (rl >= nr) break;
-    const double* e = gt + size_t(h) * S + r;
-    float lg[4];
-    double ug[4];
-    int ok = 1;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      ok &= int(gamma_fast(cv[k], cl[k], lv[k], dv[k], t0[k][rl], e + k * sl, plane, lg[k], ug[k]));
-    if (ok) {
-      tile[0][rl][lane] = beta_from_logs(aa, ab, 2.0, 5.0, lg[0], ug[0], lg[1], ug[1]);
-      tile[1][rl][lane] = beta_from_logs(sa, sb, 2.0, 5.0, lg[2], ug[2], lg[3], ug[3]);
-    } else if (lane < nc) {  // undecided in fp32 or more attempts than tabulated: k_beta_fix writes it
-      const unsigned slot = atomicAdd(p.bfix_n, 1u);
-      p.bfix[slot] = (b * uint32_t(H) + uint32_t(h)) * uint32_t(S) + uint32_t(r);
+  // kBpChunks chunks of kBpRows rows, one after another through the same LDS
+  for (int ch = 0; ch < kBpChunks; ++ch) {
+    const int r0 = (blockIdx.x * kBpChunks + ch) * kBpRows;
+    if (r0 >= S) break;  // workgroup-uniform
+    const int nr = min(kBpRows, S - r0);
+    if (ch > 0) __syncthreads();  // the previous chunk's tile and table reads are done
+    for (int q = threadIdx.x; q < 4 * kBpRows; q += blockDim.x) {  // attempt 0, streams acc A/B, steer A/B
+      const int k = q / kBpRows, rl = q - k * kBpRows;
+      const double* e = gt + k * sl + size_t(h) * S + r0 + min(rl, nr - 1);
+      t0[k][rl] = tab0_of(e, plane);
     }
-  }
-  __syncthreads();
-  for (int q = threadIdx.x; q < nc * 2 * kBpRows; q += blockDim.x) {
-    const int rl = q & (kBpRows - 1), kc = q / kBpRows, k = kc & 1, cl = kc >> 1;
-    if (rl >= nr) continue;
-    p.bplane[(size_t(g) * p.B + j0 + cl) * 2 * H * S + (size_t(k) * H + h) * S + r0 + rl] = tile[k][rl][cl];
+    __syncthreads();
+    for (int i = 0; i < kBpRows / 4; ++i) {
+      const int rl = w * (kBpRows / 4) + i, r = r0 + rl;
+      if (rl >= nr) break;
+      const double* e = gt + size_t(h) * S + r;
+      float lg[4];
+      double ug[4];
+      int ok = 1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        ok &= int(gamma_fast(cv[k], cl[k], lv[k], dv[k], t0[k][rl], e + k * sl, plane, lg[k], ug[k]));
+      if (ok) {
+        tile[0][rl][lane] = beta_from_logs(aa, ab, 2.0, 5.0, lg[0], ug[0], lg[1], ug[1]);
+        tile[1][rl][lane] = beta_from_logs(sa, sb, 2.0, 5.0, lg[2], ug[2], lg[3], ug[3]);
+      } else if (lane < nc) {  // undecided in fp32 or more attempts than tabulated: k_beta_fix writes it
+        const unsigned slot = atomicAdd(p.bfix_n, 1u);
+        p.bfix[slot] = (b * uint32_t(H) + uint32_t(h)) * uint32_t(S) + uint32_t(r);
+      }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < nc * 2 * kBpRows; q += blockDim.x) {
+      const int rl = q & (kBpRows - 1), kc = q / kBpRows, k = kc & 1, cl2 = kc >> 1;
+      if (rl >= nr) continue;
+      p.bplane[(size_t(g) * p.B + j0 + cl2) * 2 * H * S + (size_t(k) * H + h) * S + r0 + rl] = tile[k][rl][cl2];
+    }
   }
 }
 
@@ -763,7 +771,9 @@ void launch_beta_planes(const Params& p, int t, hipStream_t s) {
     const int groups = (p.B + 63) / 64;
     // the last step's draws move nothing (k_risk_baseline never applies them):
     // not drawn, except for the parity tests' plane dump
-    hipLaunchKernelGGL(k_beta_planes_c, dim3((p.S + kBpRows - 1) / kBpRows, p.beta_dump ? p.H : p.H - 1, p.G * groups),
+    hipLaunchKernelGGL(k_beta_planes_c,
+                       dim3((p.S + kBpRows * kBpChunks - 1) / (kBpRows * kBpChunks), p.beta_dump ? p.H : p.H - 1,
+                            p.G * groups),
                        dim3(256), 0, s, p, t);
   }
   hipLaunchKernelGGL(k_beta_fix, dim3(1024), dim3(256), 0, s, p, t);
