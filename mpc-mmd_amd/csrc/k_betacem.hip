@@ -709,17 +709,19 @@ constexpr int sample_waves() {
 
 DEVI d4 mfma64(double a, double b, d4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
 
-// Operands of one block, loaded unconditionally (generators, means and
-// normals are zero padded to whole blocks and tiles; features >= 11 masked
-// by selects), so the loop has no branches and the compiler can count
-// outstanding loads exactly.
+// Operands of one block, loaded unconditionally (generators and normals are
+// zero padded to whole blocks and tiles), so the loop has no branches and the
+// compiler can count outstanding loads exactly.  Generator rows (k_belite,
+// k_bgen): W plane = w_0..w_10 and a zero slot 11, U plane = u_0..u_10 and the
+// position's mean in slot 11, genm = L_jj.  With row 11 of S_pre held at 1
+// (and row 11 of S_loc exactly 0, W's slot 11 being 0), U S carries the mean
+// as its twelfth term: no mean operand, no accumulator initialisation.
 template <int TPW>
 struct SampleBlock {
   double wA[4];  // W[p0 + 4k + h][r]        (A of W^T Z; r = feature)
   double wX[3];  // W[p0 + r][4i + h]        (A of W U^T; 4i + h = feature)
-  double uX[3];  // U[p0 + r][4i + h]        (B of W U^T, A of U S)
+  double uX[3];  // U[p0 + r][4i + h]        (B of W U^T, A of U S; feature 11 = mean)
   double L;      // L_jj of position p0 + r
-  double m[4];   // mean of position p0 + h + 4i
   float z[TPW][4];   // Z[p0 + 4k + h][sample of (tile t, lane r)] (sample_of); fp32 normals, widened at use
 };
 
@@ -732,12 +734,10 @@ DEVI void load_block(SampleBlock<TPW>& q, const double* G, const double* GU, con
   const double* gu = GU + size_t(p0 + r) * kGenRow;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    q.wX[i] = g[kGenW + 4 * i + h];  // feature 11 reads L_jj, times U's zero feature 11
+    q.wX[i] = g[kGenW + 4 * i + h];  // W's zero slot 11 times U's mean: X gets no mean term
     q.uX[i] = gu[4 * i + h];
   }
-  q.L = g[kGenL];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) q.m[i] = gm[p0 + h + 4 * i];
+  q.L = gm[p0 + r];
   // tiles in pairs: lane r of tiles 2u, 2u + 1 takes samples 32u + 2r, 32u +
   // 2r + 1 -- the lane image of bz_index, six float4 loads per block (one
   // tile per wave: lane r takes sample s0 + r, scalar loads)
@@ -760,10 +760,63 @@ DEVI void load_block(SampleBlock<TPW>& q, const double* G, const double* GU, con
   }
 }
 
+// load_block<kSampleTiles> as raw buffer loads: the lane parts of the offsets
+// are fixed for the launch (four VGPRs), the block part p0 goes in SGPRs, so
+// a block's 17 loads need no per-lane address arithmetic and no 64-bit
+// address registers (the walker runs at 1 wave per SIMD, where every VALU
+// instruction and register counts).  Same addresses as load_block.
+struct SampleRsrc {
+  __amdgpu_buffer_rsrc_t gen, genm, z;
+  int vA, vX, vL, vZ;  // lane offsets (bytes): W^T rows, W / U rows, L_jj, normals
+  int uplane;          // bytes from the W plane to the U plane
+};
+DEVI SampleRsrc sample_rsrc(const double* G, const double* gm, const float* z, int Pp, int r, int h) {
+  SampleRsrc s;
+  s.gen = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(G), short(0), Pp * kGenStride * 8, 0x00020000);
+  s.genm = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(gm), short(0), Pp * 8, 0x00020000);
+  s.z = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(z), short(0), Pp * kBzCols * 4, 0x00020000);
+  s.vA = (h * kGenRow + kGenW + r) * 8;
+  s.vX = (r * kGenRow + h) * 8;
+  s.vL = r * 8;
+  s.vZ = (r + 16 * h) * 16;
+  s.uplane = Pp * kGenRow * 8;
+  return s;
+}
+DEVI double buf_ld_d(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+}
+DEVI void load_block_buf(SampleBlock<kSampleTiles>& q, const SampleRsrc& s, int p0) {
+  const int sg = p0 * kGenRow * 8;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) q.wA[k] = buf_ld_d(s.gen, s.vA + k * 4 * kGenRow * 8, sg);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    q.wX[i] = buf_ld_d(s.gen, s.vX + 32 * i, sg);
+    q.uX[i] = buf_ld_d(s.gen, s.vX + 32 * i, sg + s.uplane);
+  }
+  q.L = buf_ld_d(s.genm, s.vL, p0 * 8);
+  const int szz = (p0 >> 4) * (16 * kBzCols * 4);
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f f = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(s.z, s.vZ + 1024 * (c % 3), szz + 3072 * (c / 3), 0));
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int idx = 4 * c + w, k = idx / 6, t = idx % 6;
+      q.z[t][k] = f[w];
+    }
+  }
+}
+
 // One block's MFMAs for the wave's tiles, all accumulating in place:
-//   Y  = m + U S          (3 per tile, C operand starts at the means)
+//   Y  = U S              (3 per tile from a zero C operand; the mean is
+//                          U's feature 11 times row 11 of S_pre, which is 1)
 //   S += W^T Z            (4 per tile; after U S has read S)
 //   Y += T Z              (4 per tile; T from X = W U^T, built meanwhile)
+// The Y products are formed transposed, Y^T = S^T U^T + Z^T T^T (the same
+// operand registers with A and B exchanged), so register i of lane (r, h)
+// holds sample row h + 4i of the tile at position p0 + r: a store covers
+// four sample rows x 16 consecutive positions, no transpose before it.
 // Tiles are interleaved, so every accumulator chain has 6 MFMAs between
 // dependent steps.  No VALU work on the accumulators: the pipe never waits
 // for a vector add between blocks.
@@ -777,7 +830,7 @@ DEVI void block_mfma(const SampleBlock<TPW>& cur, d4* S, const d4* Sp, d4* Y, in
   d4 X = d4{0.0, 0.0, 0.0, 0.0};  // X = W_c U_c^T: register i holds w_{h+4i} . u_r = T[row r][col h + 4i]
 #pragma unroll
   for (int i = 0; i < 3; ++i) X = mfma64(cur.wX[i], cur.uX[i], X);
-  const d4 m = d4{cur.m[0], cur.m[1], cur.m[2], cur.m[3]};
+  const d4 zero = d4{0.0, 0.0, 0.0, 0.0};
   // B operand of U S: S_pre + S_loc (rows 0..11 of S: registers 0..2)
   double St[TPW][3];
 #pragma unroll
@@ -787,12 +840,12 @@ DEVI void block_mfma(const SampleBlock<TPW>& cur, d4* S, const d4* Sp, d4* Y, in
 #pragma unroll
   for (int k = 0; k < 3; ++k)
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) Y[t] = mfma64(cur.uX[k], St[t][k], k == 0 ? m : Y[t]);
+    for (int t = 0; t < TPW; ++t) Y[t] = mfma64(St[t][k], cur.uX[k], k == 0 ? zero : Y[t]);
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
     for (int t = 0; t < TPW; ++t) S[t] = mfma64(cur.wA[k], zd[t][k], S[t]);
-  double T[4];  // A operand of T Z, k-step i: T[r][4i + h]
+  double T[4];  // B operand of (T Z)^T, k-step i: T[r][4i + h]
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int k = h + 4 * i;
@@ -801,33 +854,54 @@ DEVI void block_mfma(const SampleBlock<TPW>& cur, d4* S, const d4* Sp, d4* Y, in
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) Y[t] = mfma64(T[k], zd[t][k], Y[t]);
+    for (int t = 0; t < TPW; ++t) Y[t] = mfma64(zd[t][k], T[k], Y[t]);
 }
 
-// the finished block's samples to fp32 (the sigma coordinate M clipped)
-// Register i of lane row h holds position p0 + h + 4i; a 4 x 4 transpose
-// across (lane row, register) -- a block swap by permlane32, then the 2 x 2
-// blocks by permlane16 -- leaves positions p0 + 4h .. p0 + 4h + 3 in lane row
-// h, stored as one 16-byte write per tile.
-// Blocks wholly past the sigma coordinate and the padding samples >= kNew of
-// the last tile are not stored (k_bselect never reads them).
+// the finished block's samples to fp32 (the sigma coordinate M clipped).
+// Lane (r, h), register i of tile t: sample row rho = h + 4i of the tile
+// (sample s0 + rho for one tile per wave; 32 (t / 2) + 2 rho + t % 2 for the
+// paired tiles of the one-wave walker), position p0 + r; per store, four
+// sample rows x 64 contiguous bytes.  Blocks wholly past the sigma coordinate
+// and the padding samples >= kNew are not stored (k_bselect never reads them).
+HDI_CONST int tile_sample(int TPW, int s0, int t, int rho) { return TPW == 1 ? s0 + rho : 32 * (t >> 1) + 2 * rho + (t & 1); }
 template <int TPW>
-DEVI void block_store(const d4* Yv, float* Y, int p0, int M, int ys, int sl, int h) {
+DEVI void block_store(const d4* Yv, float* plane, int p0, int M, int ys, int s0, int r, int h) {
   if (p0 > M) return;
 #pragma unroll
-  for (int t = 0; t < TPW; ++t) {
-    float v[4];
+  for (int t = 0; t < TPW; ++t)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = p0 + h + 4 * i == M ? fmaxf(float(Yv[t][i]), 0.01f) : float(Yv[t][i]);
-    permlane_swap<32>(v[0], v[2]);
-    permlane_swap<32>(v[1], v[3]);
-    permlane_swap<16>(v[0], v[1]);
-    permlane_swap<16>(v[2], v[3]);
-    // sample s0 + 32 (t / 2) + 2 r + t % 2 (one tile per wave: s0 + r)
-    const int so = TPW == 1 ? 0 : 32 * (t >> 1) + (t & 1);
-    float4* yrow = reinterpret_cast<float4*>(Y + size_t(so) * ys + p0 + 4 * h);
-    if (sl + so < kNew) *yrow = make_float4(v[0], v[1], v[2], v[3]);  // sl: the lane's sample of tile 0
-  }
+    for (int i = 0; i < 4; ++i) {
+      const int s = tile_sample(TPW, s0, t, h + 4 * i);
+      const float v = float(Yv[t][i]);
+      if (s < kNew) plane[size_t(s) * ys + p0 + r] = p0 + r == M ? fmaxf(v, 0.01f) : v;
+    }
+}
+
+// k_bsample's store of a finished block that does not hold the sigma
+// coordinate M: block_store<kSampleTiles> without the clip's selects and
+// without per-block address arithmetic (on gfx950 a wave's VALU work does not
+// run in the shadow of its fp64 MFMAs -- tools/mfma_overlap.hip: +6..8
+// clocks per VALU instruction between MFMAs).  Raw buffer stores over the
+// candidate's sample plane: the lane part of the offset (vl = row 2h,
+// position r) is fixed for the launch, the block, tile and register parts go
+// in an SGPR.  Tiles 0-3 hold real samples only; in tiles 4 and 5 register 3
+// holds samples 88 + 2h + t % 2 >= kNew but for (t = 4, h = 0) -- that store
+// takes v43, out of range (dropped by the buffer unit) for h > 0, and tile
+// 5's register 3 is not stored.
+DEVI __amdgpu_buffer_rsrc_t ygen_rsrc(float* plane, int ys) {
+  return __builtin_amdgcn_make_buffer_rsrc(plane, short(0), kBzCols * ys * 4, 0x00020000);
+}
+constexpr int kDropOffset = 0x7FFFFF00;  // out of range for any plane
+static_assert(kNew == 89, "tile 4 / 5 register 3 validity below");
+DEVI void block_store_rows(const d4* Yv, __amdgpu_buffer_rsrc_t yr, int p0, int ys, int vl, int v43) {
+#pragma unroll
+  for (int t = 0; t < kSampleTiles; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (t == 5 && i == 3) continue;
+      const int soff = ((32 * (t >> 1) + (t & 1) + 8 * i) * ys + p0) * 4;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(float(Yv[t][i])), yr, t == 4 && i == 3 ? v43 : vl, soff, 0);
+    }
 }
 
 // S_pre += S_loc, S_loc = 0 (a chunk's end)
@@ -848,37 +922,54 @@ __global__ __launch_bounds__(64 * sample_waves<TPW>()) void k_bsample(Params p, 
   const double* gm = p.genm + size_t(b) * Pp;
   const float* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
   const int ys = ygen_stride(M);
-  const int sl = s0 + (TPW == 1 ? r : 2 * r);
-  float* Y = p.ygen + (size_t(b) * kBzCols + sl) * ys;
+  float* plane = p.ygen + size_t(b) * kBzCols * ys;
   d4 S[TPW], Sp[TPW], Ya[TPW], Yb[TPW];
 #pragma unroll
-  for (int t = 0; t < TPW; ++t) S[t] = Sp[t] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int t = 0; t < TPW; ++t) {
+    S[t] = Sp[t] = d4{0.0, 0.0, 0.0, 0.0};
+    Sp[t][2] = h == 3 ? 1.0 : 0.0;  // row 11 of S_pre: the mean's coefficient
+  }
   const int nblk = Pp >> 4, cl = sample_chunk(nblk);
+  const __amdgpu_buffer_rsrc_t yr = ygen_rsrc(plane, ys);
+  const int vl = (2 * h * ys + r) * 4, v43 = h == 0 ? vl : kDropOffset;
+  auto store = [&](const d4* Yv, int q0) {
+    if (TPW == kSampleTiles && q0 + 15 < M)  // block-uniform
+      block_store_rows(Yv, yr, q0, ys, vl, v43);
+    else
+      block_store<TPW>(Yv, plane, q0, M, ys, s0, r, h);
+  };
   // blocks in pairs, operands and outputs ping-ponged: the next block's loads
   // are in flight and its MFMAs issued while the previous block's samples
   // are converted and stored (the last prefetch re-reads a block; nblk and
   // the chunk length are even; sched barriers keep that order)
   SampleBlock<TPW> qa, qb;
-  load_block(qa, G, G + gen_uplane(Pp), gm, z, 0, s0, r, h);
+  const SampleRsrc srs = sample_rsrc(G, gm, z, Pp, r, h);
+  auto load = [&](SampleBlock<TPW>& q, int q0) {
+    if constexpr (TPW == kSampleTiles)
+      load_block_buf(q, srs, q0);
+    else
+      load_block(q, G, G + gen_uplane(Pp), gm, z, q0, s0, r, h);
+  };
+  load(qa, 0);
   for (int c = 0; c < nblk; c += 2) {
     const int p0 = c << 4;
-    load_block(qb, G, G + gen_uplane(Pp), gm, z, p0 + 16, s0, r, h);
+    load(qb, p0 + 16);
     __builtin_amdgcn_sched_barrier(0);
     block_mfma(qa, S, Sp, Ya, r, h);
     __builtin_amdgcn_sched_barrier(0);
-    if (c > 0) block_store<TPW>(Yb, Y, p0 - 16, M, ys, sl, h);
+    if (c > 0) store(Yb, p0 - 16);
     __builtin_amdgcn_sched_barrier(0);
-    load_block(qa, G, G + gen_uplane(Pp), gm, z, min(p0 + 32, Pp - 16), s0, r, h);
+    load(qa, min(p0 + 32, Pp - 16));
     __builtin_amdgcn_sched_barrier(0);
     block_mfma(qb, S, Sp, Yb, r, h);
     if ((c + 2) % cl == 0)
 #pragma unroll
       for (int t = 0; t < TPW; ++t) fold_chunk(Sp[t], S[t]);
     __builtin_amdgcn_sched_barrier(0);
-    block_store<TPW>(Ya, Y, p0, M, ys, sl, h);
+    store(Ya, p0);
     __builtin_amdgcn_sched_barrier(0);
   }
-  block_store<TPW>(Yb, Y, Pp - 16, M, ys, sl, h);
+  store(Yb, Pp - 16);
   MPCMMD_STAMP(p, 1);
 }
 
@@ -898,7 +989,7 @@ __global__ __launch_bounds__(64 * kChunkWavesMax) void k_bsample_chunks(Params p
   const double* gm = p.genm + size_t(b) * Pp;
   const float* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
   const int ys = ygen_stride(M);
-  float* Y = p.ygen + (size_t(b) * kBzCols + s0 + r) * ys;
+  float* plane = p.ygen + size_t(b) * kBzCols * ys;
   if (k < P - 1) {
     // operands of W^T Z for block c: W[p0 + 4 kk + h][r], Z[p0 + 4 kk + h][s0 + r]
     auto ld = [&](double (&wa)[4], double (&zz)[4], int c) {
@@ -927,6 +1018,7 @@ __global__ __launch_bounds__(64 * kChunkWavesMax) void k_bsample_chunks(Params p
   }
   __syncthreads();
   d4 S[1] = {d4{0.0, 0.0, 0.0, 0.0}}, Sp[1] = {d4{0.0, 0.0, 0.0, 0.0}}, Ya[1], Yb[1];
+  Sp[0][2] = h == 3 ? 1.0 : 0.0;  // row 11 of S_pre: the mean's coefficient (the chunks' row 11 sums are 0)
   for (int j = 0; j < k; ++j)
 #pragma unroll
     for (int i = 0; i < 3; ++i) Sp[0][i] = Sp[0][i] + dS[j][i][lane];
@@ -939,16 +1031,16 @@ __global__ __launch_bounds__(64 * kChunkWavesMax) void k_bsample_chunks(Params p
     __builtin_amdgcn_sched_barrier(0);
     block_mfma(qa, S, Sp, Ya, r, h);
     __builtin_amdgcn_sched_barrier(0);
-    if (c > c0) block_store<1>(Yb, Y, p0 - 16, M, ys, s0 + r, h);
+    if (c > c0) block_store<1>(Yb, plane, p0 - 16, M, ys, s0, r, h);
     __builtin_amdgcn_sched_barrier(0);
     load_block(qa, G, G + gen_uplane(Pp), gm, z, min(p0 + 32, pend - 16), s0, r, h);
     __builtin_amdgcn_sched_barrier(0);
     block_mfma(qb, S, Sp, Yb, r, h);
     __builtin_amdgcn_sched_barrier(0);
-    block_store<1>(Ya, Y, p0, M, ys, s0 + r, h);
+    block_store<1>(Ya, plane, p0, M, ys, s0, r, h);
     __builtin_amdgcn_sched_barrier(0);
   }
-  block_store<1>(Yb, Y, pend - 16, M, ys, s0 + r, h);
+  block_store<1>(Yb, plane, pend - 16, M, ys, s0, r, h);
   MPCMMD_STAMP(p, 1);
 }
 
@@ -2005,7 +2097,7 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
   const int span = ((nblk * 16 + 63) / 64) * 64;  // whole waves
   for (int j = tid; j < span; j += blockDim.x) {
     const bool valid = j < M1;
-    double u[kBetaElite];
+    double u[kBetaElite], mean;
     {
       float v[kBetaElite];
       double s = 0.0;
@@ -2037,7 +2129,7 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
       const double m = s / double(kBetaElite);
 #pragma unroll
       for (int q = 0; q < kBetaElite; ++q) u[q] = valid ? (double(v[q]) - m) * rs10 : 0.0;
-      if (valid) p.genm[size_t(b) * pos_pad(M) + j] = double(float(m));
+      mean = valid ? double(float(m)) : 0.0;
     }
     // level 1: block sums G = U^T U of u u^T over each 16-position block (66
     // packed entries) on fp64 MFMA: the wave's four blocks one at a time, the
@@ -2052,7 +2144,7 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
       if ((lane >> 4) == k) {
 #pragma unroll
         for (int q = 0; q < kBetaElite; ++q) ub[(lane & 15) * kUPitch + q] = u[q];
-        ub[(lane & 15) * kUPitch + 11] = 0.0;
+        ub[(lane & 15) * kUPitch + kGenMean] = mean;  // the U row's slot 11 (the MFMA below masks it)
       }
       wave_sync();
       d4 G = d4{0.0, 0.0, 0.0, 0.0};
@@ -2065,10 +2157,10 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
       // on consecutive features of a row, so a store instruction covers ~6
       // position rows (a lane per position wrote 64 rows per instruction)
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int e = lane + 64 * i, row = e / kBetaElite, q = e - row * kBetaElite;
+      for (int i = 0; i < 3; ++i) {  // whole rows: u_0..u_10 and the mean
+        const int e = lane + 64 * i, row = e / kGenRow, q = e - row * kGenRow;
         const int pos = blk * 16 + row;
-        if (e < 16 * kBetaElite && pos < M1) gen[gen_uplane(pos_pad(M)) + size_t(pos) * kGenRow + q] = ub[row * kUPitch + q];
+        if (pos < M1) gen[gen_uplane(pos_pad(M)) + size_t(pos) * kGenRow + q] = ub[row * kUPitch + q];
       }
       wave_sync();
       // register i: G[h + 4 i][r]; the packed upper triangle a <= c
@@ -2196,9 +2288,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     double* g = gen + size_t(j) * kGenRow;
     if (live) {
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
-        if (q + 4 * i < 11) g[kGenW + q + 4 * i] = w[i];
-      if (q == 0) g[kGenL] = ljj;
+      for (int i = 0; i < 3; ++i) g[kGenW + q + 4 * i] = q + 4 * i < 11 ? w[i] : 0.0;  // whole rows: slot 11 is 0
+      if (q == 0) p.genm[size_t(b) * pos_pad(M) + j] = ljj;
     }
 #pragma unroll
     for (int c = 0; c < 11; ++c) {
@@ -2248,7 +2339,7 @@ __global__ __launch_bounds__(kThreads) void k_bsigma(Params p, int tb) {
         d += gu[a] * sa;
       }
       const double zM = z[bz_index(M, si)];
-      const float yM = float((p.genm[size_t(b) * pos_pad(M) + M] + g[kGenL] * zM) + d);
+      const float yM = float((gu[kGenMean] + p.genm[size_t(b) * pos_pad(M) + M] * zM) + d);
       p.sigma[b] = fmaxf(yM, 0.01f);
     }
   }

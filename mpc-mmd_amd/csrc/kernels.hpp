@@ -18,17 +18,16 @@ constexpr int kBetaElite = 11;         // compute_beta.py:26
 constexpr int kEliteCost = 20;         // cem.py:140
 constexpr int kElite = 5;              // cem.py:138
 constexpr int kResultStride = 11 + 11 + 2 + 1 + 20 + kMaxReduced;  // cx, cy, lane, obs, sigma, res_beta, beta
-// doubles per position in Params::gen: W 0..10, zeros 11..14, L_jj 15,
-// U 16..26, zeros 27..31 (the zero slots are the padding features of the
-// 16x16x4 MFMA operands, so the sampling kernel loads them unmasked)
 // generators per candidate: two planes of pos_pad(M) rows x kGenRow doubles,
-// W (features 0..10, L_jj in the feature-11 slot: the sampler's K padding
-// multiplies it by U's zero feature 11) then U (features 0..10, slot 11 zero).
-// 192 B per position (the r02 row of 256 B held both with padding); planes,
-// not interleaved rows, so k_bgen's U reads and W writes never share a line.
+// W (features 0..10, slot 11 zero) then U (features 0..10, the position's
+// fp32-rounded elite mean in slot 11), and L_jj in Params::genm.  The sampler
+// feeds slot 11 through the 16x16x4 MFMA operands unmasked: W's zero slot
+// keeps the mean out of W U^T, and row 11 of its S_pre is 1, so U S adds the
+// mean.  192 B per position; planes, not interleaved rows, so k_bgen's U
+// reads and W writes never share a line.
 constexpr int kGenRow = 12;
 constexpr int kGenStride = 2 * kGenRow;  // doubles per position and candidate
-constexpr int kGenW = 0, kGenL = 11;
+constexpr int kGenW = 0, kGenMean = 11;
 HDI_CONST size_t gen_uplane(int Pp) { return size_t(Pp) * kGenRow; }  // U plane offset
 HDI_CONST int ygen_stride(int M) { return ((M + 1) + 31) & ~31; }
 // beta-CEM sample generation works on pairs of blocks of 16 positions and
@@ -146,7 +145,7 @@ struct Params {
   double* gen;             // [B][W, U plane][pos_pad(M)][kGenRow] (pad rows 0)
   double* phib;            // [B][ceil((M+1)/16)][66] Phi at the start of each 16-position block
   int32_t* bimin;          // [B] argmin sample of the last beta-iteration
-  double* genm;            // [B][pos_pad(M)]  fp32-rounded elite mean, as fp64 (pad 0)
+  double* genm;            // [B][pos_pad(M)]  L_jj of the generators (pad 0)
   int32_t* bestsel;        // [B][n]       reduced set of the best sample
   float* brow;             // [B][100][n]  K_mixed row sums (fp32 partial sums, the reference's precision)
   float* bkred;            // [B][100][tri_stride(n)] K_red strict lower triangle (entry (k, kk < k) at k (k-1)/2 + kk)
