@@ -17,6 +17,7 @@
 #include <cstdlib>
 
 #include "block.hpp"
+#include "draws.hpp"
 #include "kernels.hpp"
 #include "rng.hpp"
 #include "rollout.hpp"
@@ -204,25 +205,10 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
 }
 
 // Beta-noise attempt table of outer iteration t (rng.hpp): one thread per
-// (stream, attempt, r, h)
+// (stream, attempt, r, h) of configuration blockIdx.y (draws.hpp)
 __global__ __launch_bounds__(256) void k_gamma_tab(Params p, int t) {
-  const int S = p.S, H = p.H;
-  const int plane = S * H;
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  const Cfg cf = cfg_of(p, blockIdx.y);
-  if (idx == 0 && blockIdx.y == 0) *p.bfix_n = 0u;  // k_beta_planes' deferred list of this iteration
-  if (idx >= kGammaTabStreams * kGammaTabAttempts * plane) return;
-  const int e = idx % plane, sk = idx / plane;
-  const int k = sk % kGammaTabAttempts, st = sk / kGammaTabAttempts;
-  const int h = e / S, r = e - h * S;
-  const uint32_t k0 = iteration_key0(cf.idx_mpc, t), k1 = p.seed;
-  const GammaAttempt g = gamma_attempt(k0, k1, kStreamGammaAccA + uint32_t(st), uint32_t(r) * uint32_t(H) + h, k);
-  double* o = cf.gtab + (size_t(sk) * 4) * plane + e;
-  o[0] = g.x;
-  o[plane] = g.u;
-  o[2 * size_t(plane)] = g.lu;
-  const bool squeeze = g.u < 1.0 - 0.0331 * (g.x * g.x) * (g.x * g.x);  // alpha-independent (rng.hpp)
-  o[3 * size_t(plane)] = squeeze ? g.lw : -g.lw;
+  if (idx < gamma_items(p)) gamma_item(p, t, cfg_of(p, blockIdx.y), idx);
 }
 
 // Beta draws of every (candidate, row, step) of the baseline rollouts,
@@ -780,7 +766,7 @@ void launch_beta_planes(const Params& p, int t, hipStream_t s) {
 }
 
 void launch_gamma_tab(const Params& p, int t, hipStream_t s) {
-  const int total = kGammaTabStreams * kGammaTabAttempts * p.S * p.H;
+  const int total = gamma_items(p);
   hipLaunchKernelGGL(k_gamma_tab, dim3((total + 255) / 256, p.G), dim3(256), 0, s, p, t);
 }
 

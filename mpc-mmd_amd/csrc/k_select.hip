@@ -10,6 +10,7 @@
 //
 // Plus stage "noise": the internal Philox draws of one outer iteration.
 #include "block.hpp"
+#include "draws.hpp"
 #include "kernels.hpp"
 #include "rng.hpp"
 
@@ -27,7 +28,9 @@ DEVI void wave_sync_lds() {
 constexpr int kMaxSortN = 4096;
 constexpr int kN = 100;
 
-__global__ __launch_bounds__(1024) void k_select(Params p, int t) {
+// Workgroups G.. (when kind != 0) draw iteration ahead_t's noise / gamma
+// table items (draws.hpp) meanwhile.
+__global__ __launch_bounds__(1024) void k_select(Params p, int t, int ahead_t, int kind) {
   __shared__ __attribute__((aligned(16))) unsigned long long keys[kMaxSortN];
   __shared__ int perm[kMaxSortN];
   __shared__ int el[kEliteCost];
@@ -38,6 +41,10 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
   __shared__ double cvs[8][8];
   __shared__ float mean32[8];
   __shared__ int imin_s;
+  if (int(blockIdx.x) >= p.G) {  // whole workgroups: no barrier below is reached
+    ahead_item(p, ahead_t, kind, (int(blockIdx.x) - p.G) * 1024 + int(threadIdx.x));
+    return;
+  }
   const int B = p.B;
   const Cfg cf = cfg_of(p, blockIdx.x);  // one workgroup per configuration
   const int g0 = blockIdx.x * B;          // its first candidate
@@ -292,45 +299,19 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t) {
 
 // internal draws of outer iteration t: roll [3][H][S] and resample [B-5][8]
 __global__ __launch_bounds__(256) void k_noise(Params p, int t) {
-  const int S = p.S, H = p.H;
-  const Cfg cf = cfg_of(p, blockIdx.y);  // configuration blockIdx.y, keyed by its own idx_mpc
-  const uint32_t k0 = iteration_key0(cf.idx_mpc, t), k1 = p.seed;
-  const int nroll = (S * H + 3) / 4;
-  const int nres = ((p.B - kElite) * 8 + 3) / 4;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  float* roll = const_cast<float*>(cf.roll) + size_t(t) * 3 * H * S;
-  float* res = const_cast<float*>(cf.resample) + size_t(t) * (p.B - kElite) * 8;
-  if (j < 3 * nroll) {
-    const int st = j / nroll, jb = j % nroll;
-    double z[4];
-    philox_normals4(k0, k1, kStreamRollAcc + st, 0u, uint32_t(jb), z);
-    for (int q = 0; q < 4; ++q) {
-      const int e = 4 * jb + q;
-      if (e >= S * H) break;
-      const int s = e / H, h = e % H;
-      roll[(size_t(st) * H + h) * S + s] = float(z[q]);
-    }
-  } else if (j < 3 * nroll + nres) {
-    const int jb = j - 3 * nroll;
-    double z[4];
-    philox_normals4(k0, k1, kStreamResample, 0u, uint32_t(jb), z);
-    for (int q = 0; q < 4; ++q) {
-      const int e = 4 * jb + q;
-      if (e < (p.B - kElite) * 8) res[e] = float(z[q]);
-    }
-  }
+  if (j < noise_items(p)) noise_item(p, t, cfg_of(p, blockIdx.y), j);  // configuration blockIdx.y
 }
 
 }  // namespace
 
-void launch_select(const Params& p, int t, hipStream_t s) {
-  hipLaunchKernelGGL(k_select, dim3(p.G), dim3(1024), 0, s, p, t);
+void launch_select(const Params& p, int t, hipStream_t s, int ahead_t, int kind) {
+  const int extra = ahead_t >= 0 && kind ? (p.G * ahead_items(p, kind) + 1023) / 1024 : 0;
+  hipLaunchKernelGGL(k_select, dim3(p.G + extra), dim3(1024), 0, s, p, t, ahead_t, extra ? kind : 0);
 }
 
 void launch_noise(const Params& p, int t, hipStream_t s) {
-  const int nroll = (p.S * p.H + 3) / 4;
-  const int nres = ((p.B - kElite) * 8 + 3) / 4;
-  const int total = 3 * nroll + nres;
+  const int total = noise_items(p);
   hipLaunchKernelGGL(k_noise, dim3((total + 255) / 256, p.G), dim3(256), 0, s, p, t);
 }
 

@@ -224,7 +224,9 @@ __device__ inline Cfg cfg_of(const Params& p, int g) {
 
 void launch_noise(const Params& p, int t, hipStream_t s);
 void launch_front(const Params& p, int t, hipStream_t s);
-void launch_select(const Params& p, int t, hipStream_t s);
+// ahead_t >= 0: the launch also draws iteration ahead_t's items of `kind`
+// (draws.hpp: kAheadNoise | kAheadGamma) in spare workgroups
+void launch_select(const Params& p, int t, hipStream_t s, int ahead_t = -1, int kind = 0);
 void launch_risk_baseline(const Params& p, int t, hipStream_t s);
 // the same risk with candidate lanes and the Beta draws inside the rollouts
 // (k_mt_tab, k_roll_cand, k_risk_reduce): Params::risk_rows = 0 (MPCMMD_RISK_FUSED=1)

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "carla_host.hpp"
+#include "draws.hpp"
 #include "host_constants.hpp"
 #include "kernels.hpp"
 #include "rng.hpp"
@@ -117,7 +118,16 @@ struct mpcmmd_handle {
   // length, external draws, configurations) and replayed (one hipGraphLaunch
   // instead of ~150 launches per outer iteration)
   bool graphs = false;
-  std::map<std::tuple<int, int, int, int, int, int>, std::pair<hipGraph_t, hipGraphExec_t>> gexec;
+  using GraphKey = std::tuple<int, int, int, int, int, int, int>;
+  std::map<GraphKey, std::pair<hipGraph_t, hipGraphExec_t>> gexec;
+  std::map<GraphKey, int> gahead;  // ahead_t after the captured iterations ran
+  // draws ahead: k_select of iteration t also draws iteration t + 1's noise
+  // and Beta attempt table (draws.hpp); ahead_t = the iteration whose draws
+  // are already on the device that way (-1: none).  Deterministic draws, so
+  // producing them early changes no value; invalidated by begin and by any
+  // gamma table drawn for another iteration (the table has one slot)
+  bool ahead_on = true;
+  int ahead_t = -1;
   // profiling
   bool prof = false;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -358,17 +368,30 @@ void run_carla_risk(mpcmmd_handle* h, int t, int mode) {
   h->launch(kKRiskCarla, [&] { launch_risk_carla(p, t, mode, h->stream); });
 }
 
+// the draws k_select produces ahead for this solve (mpcmmd_handle::ahead_t)
+int ahead_kind(const mpcmmd_handle* h) {
+  if (!h->ahead_on) return 0;
+  return (h->ext_roll && h->ext_res ? 0 : kAheadNoise) | (h->p.noise == MPCMMD_NOISE_BETA ? kAheadGamma : 0);
+}
+
+// the Beta attempt table of iteration t, unless k_select of t - 1 drew it
+void ensure_gamma_tab(mpcmmd_handle* h, int t) {
+  if (h->p.noise != MPCMMD_NOISE_BETA || h->ahead_t == t) return;
+  h->launch(kKGammaTab, [&] { launch_gamma_tab(h->p, t, h->stream); });
+  h->ahead_t = -1;  // the table's one slot now holds t
+}
+
 void run_stage(mpcmmd_handle* h, int stage, int t) {
   const Params& p = h->p;
   switch (stage) {
     case 0:
-      h->launch(kKNoise, [&] { launch_noise(p, t, h->stream); });
+      if (!(h->ahead_t == t && (ahead_kind(h) & kAheadNoise))) h->launch(kKNoise, [&] { launch_noise(p, t, h->stream); });
       break;
     case 1:
       h->launch(kKFront, [&] { launch_front(p, t, h->stream); });
       break;
     case 2:
-      if (p.noise == MPCMMD_NOISE_BETA) h->launch(kKGammaTab, [&] { launch_gamma_tab(p, t, h->stream); });
+      ensure_gamma_tab(h, t);
       if (p.cost == MPCMMD_COST_MMD_OPT) {
         if (!h->mmd_ok) throw std::invalid_argument("mmd_opt unsupported for this configuration: " + h->mmd_why);
         ensure_sel0(h);
@@ -389,9 +412,12 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
         h->launch(kKRiskBaseline, [&] { launch_risk_baseline(p, t, h->stream); });
       }
       break;
-    case 3:
-      h->launch(kKSelect, [&] { launch_select(p, t, h->stream); });
+    case 3: {
+      const int kind = ahead_kind(h), nxt = kind && t + 1 < h->T ? t + 1 : -1;
+      h->launch(kKSelect, [&] { launch_select(p, t, h->stream, nxt, kind); });
+      h->ahead_t = nxt;
       break;
+    }
     case 4:
     case 5:
     case 6:
@@ -400,7 +426,7 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
       if (p.cost != MPCMMD_COST_MMD_OPT || !h->mmd_ok) throw std::invalid_argument("stages 4-8 need cost mmd_opt");
       if (stage >= 5 && stage <= 7 && t >= kBetaIters) throw std::invalid_argument("beta-CEM iteration out of range");
       if (stage == 4) {  // mother rollouts, features and their distance matrix
-        if (p.noise == MPCMMD_NOISE_BETA) h->launch(kKGammaTab, [&] { launch_gamma_tab(p, t, h->stream); });
+        ensure_gamma_tab(h, t);
         ensure_sel0(h);
         h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
         h->launch(kKBDist, [&] { launch_bdist(p, h->stream); });
@@ -656,6 +682,7 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     if (BT >= 1024) h->groups = 2;
     h->groups_forced = std::getenv("MPCMMD_GROUPS") != nullptr;
     if (const char* g = std::getenv("MPCMMD_GRAPH")) h->graphs = std::atoi(g) != 0;
+    if (const char* g = std::getenv("MPCMMD_AHEAD")) h->ahead_on = std::atoi(g) != 0;
     if (const char* g = std::getenv("MPCMMD_BETA_DUMP")) p.beta_dump = std::atoi(g) != 0;
     p.risk_rows = 1;  // the row-lane path is the faster one at configs[2]; MPCMMD_RISK_FUSED=1: fused
     if (const char* g = std::getenv("MPCMMD_RISK_FUSED")) p.risk_rows = std::atoi(g) == 0;
@@ -918,6 +945,7 @@ int begin_impl(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t
     drain.armed = false;
     h->begun = true;
     h->last_t = -1;
+    h->ahead_t = -1;
     return MPCMMD_OK;
   });
 }
@@ -1002,10 +1030,13 @@ int mpcmmd_iterate(mpcmmd_handle* h, int32_t t_begin, int32_t count) {
     const bool whole = t_begin == 0 && count == h->T;
     if (h->graphs && !h->prof && one_stream && (whole || count == 1)) {
       if (h->cost == MPCMMD_COST_MMD_OPT) ensure_sel0(h);  // host read-back: never inside a capture
-      auto key_of = [&](int tb, int cnt) {
-        return std::make_tuple(h->cost, h->p.P, int(h->ext_roll), h->G, whole ? 0 : tb, cnt);
+      // key: ... and whether the first iteration's draws were drawn ahead (ai)
+      auto key_of = [&](int tb, int cnt, int ai) {
+        return std::make_tuple(h->cost, h->p.P, int(h->ext_roll), h->G, whole ? 0 : tb, cnt, ai);
       };
-      auto capture = [&](int tb, int cnt) {
+      auto capture = [&](int tb, int cnt, int ai) {
+        const int saved = h->ahead_t;
+        h->ahead_t = ai ? tb : -1;
         hipGraph_t g = nullptr;
         HIPC(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
         try {
@@ -1013,22 +1044,30 @@ int mpcmmd_iterate(mpcmmd_handle* h, int32_t t_begin, int32_t count) {
         } catch (...) {
           (void)hipStreamEndCapture(h->stream, &g);
           if (g) (void)hipGraphDestroy(g);
+          h->ahead_t = saved;
           throw;
         }
         HIPC(hipStreamEndCapture(h->stream, &g));
         hipGraphExec_t e = nullptr;
         HIPC(hipGraphInstantiate(&e, g, nullptr, nullptr, 0));
-        h->gexec.emplace(key_of(tb, cnt), std::make_pair(g, e));
+        h->gexec.emplace(key_of(tb, cnt, ai), std::make_pair(g, e));
+        h->gahead[key_of(tb, cnt, ai)] = h->ahead_t;
+        h->ahead_t = saved;
       };
-      if (h->gexec.find(key_of(t_begin, count)) == h->gexec.end()) {
+      const int ai_now = h->ahead_t == t_begin && ahead_kind(h) ? 1 : 0;
+      if (h->gexec.find(key_of(t_begin, count, ai_now)) == h->gexec.end()) {
         if (whole) {
-          capture(0, h->T);
-        } else {
-          for (int tb = 0; tb < h->T; ++tb)
-            if (h->gexec.find(key_of(tb, 1)) == h->gexec.end()) capture(tb, 1);
+          capture(0, h->T, ai_now);
+        } else {  // the in-order pattern (iteration tb's draws drawn by tb - 1), then the one asked for
+          for (int tb = 0; tb < h->T; ++tb) {
+            const int ai = tb > 0 && ahead_kind(h) ? 1 : 0;
+            if (h->gexec.find(key_of(tb, 1, ai)) == h->gexec.end()) capture(tb, 1, ai);
+          }
+          if (h->gexec.find(key_of(t_begin, 1, ai_now)) == h->gexec.end()) capture(t_begin, 1, ai_now);
         }
       }
-      HIPC(hipGraphLaunch(h->gexec.find(key_of(t_begin, count))->second.second, h->stream));
+      HIPC(hipGraphLaunch(h->gexec.find(key_of(t_begin, count, ai_now))->second.second, h->stream));
+      h->ahead_t = h->gahead[key_of(t_begin, count, ai_now)];
     } else {
       body(t_begin, count);
     }
