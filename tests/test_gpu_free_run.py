@@ -147,3 +147,41 @@ def test_iteration_graphs(native, cost, noise, n):
                 assert np.array_equal(got[k], v, equal_nan=True), f"{k} differs with graphs (run {rep})"
             else:
                 assert got[k] == v or (v != v and got[k] != got[k]), f"{k} differs with graphs (run {rep})"
+
+
+@pytest.mark.parametrize("cost,noise,n", [("cvar", "beta", 24), ("mmd_opt", "gaussian", 6)])
+def test_draws_ahead(native, cost, noise, n, monkeypatch):
+    """k_select of iteration t drawing iteration t + 1's noise and Beta attempt
+    table (MPCMMD_AHEAD, on by default) changes no bit: in order, with an
+    iteration re-run (its successor's draws come again), after a skipped
+    iteration (drawn normally), with single-iteration graphs, and across a
+    new solve whose key differs (begin drops the ahead draws)."""
+    from parity import make_pair
+    Tg = 6
+    order = [0, 1, 1, 2, 4, 5, 3]
+
+    def run(ahead, graphs, idx):
+        monkeypatch.setenv("MPCMMD_AHEAD", "1" if ahead else "0")
+        ora, nat, xo, yo = make_pair(native, cost, noise, n=n, O=O, H=10, B=B, T=Tg)
+        nat.set_graphs(graphs)
+        outs = []
+        for k in idx:
+            nat.begin(cost, k, DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, xo, yo, 15.0)
+            for t in order:
+                nat.iterate(t, 1)
+                outs.append((nat.read("pop").copy(), nat.read("obs_cost").copy()))
+            outs.append(nat.finish())
+        nat.close()
+        return outs
+
+    ref = run(False, False, [3, 7])
+    for ahead, graphs in [(True, False), (True, True)]:
+        got = run(ahead, graphs, [3, 7])
+        for i, (g, r) in enumerate(zip(got, ref)):
+            if isinstance(r, tuple):
+                assert all(np.array_equal(a, b, equal_nan=True) for a, b in zip(g, r)), \
+                    f"step {i} differs (ahead={ahead}, graphs={graphs})"
+            else:
+                for k, v in r.items():
+                    if isinstance(v, np.ndarray):
+                        assert np.array_equal(g[k], v, equal_nan=True), f"{k} differs (ahead={ahead}, graphs={graphs})"
