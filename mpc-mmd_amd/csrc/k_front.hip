@@ -122,6 +122,28 @@ DEVI Polar polar_of(float alpha, float wx, float wy, float lo, float hi) {
   return Polar{ca, sa, d};
 }
 
+// Two wave-uniform GEMVs out_x[k] = float(cx0[k] + sum_j Ax[k][j] x[j]) and
+// out_y likewise (fp64, j in order): a row per lane (lanes k and 16 + k; the
+// rest repeat row 10) and the 22 results broadcast by readlane -- the same
+// operations in the same order as every lane forming all 22 sums, with a
+// tenth of the VALU instructions (k_front runs one wave per SIMD, where each
+// instruction is exposed).
+template <int NJ>
+DEVI void gemv2_rows(const double* cx0, const double* cy0, const double* Ax, const double* Ay, const double (&x)[NJ],
+                     const double (&y)[NJ], float (&ox)[kNv], float (&oy)[kNv]) {
+  const int lane = threadIdx.x & 63, sel = (lane >> 4) & 1, k = min(lane & 15, kNv - 1);
+  const double* A = (sel ? Ay : Ax) + k * NJ;
+  double s = (sel ? cy0 : cx0)[k];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) s += A[j] * (sel ? y[j] : x[j]);
+  const int f = __float_as_int(float(s));
+#pragma unroll
+  for (int q = 0; q < kNv; ++q) {
+    ox[q] = __int_as_float(__builtin_amdgcn_readlane(f, q));
+    oy[q] = __int_as_float(__builtin_amdgcn_readlane(f, 16 + q));
+  }
+}
+
 __global__ __launch_bounds__(256) void k_front(Params p, int t) {
   __shared__ float sB[3 * kN * kNv];
   extern __shared__ float sPath[];  // CARLA: arc_vec [P], kappa [P] of the candidate block's configuration
@@ -160,19 +182,15 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
   double cxb[kNv], cyb[kNv];
   float fcxb[kNv], fcyb[kNv];
   {
-    double v[8];
+    double vx[4], vy[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = double(pop[j]);
+    for (int j = 0; j < 4; ++j) {
+      vx[j] = double(pop[j]);
+      vy[j] = double(pop[4 + j]);
+    }
+    gemv2_rows<4>(solve_c, solve_c + kNv, p.guess_g, p.guess_g + kNv * 4, vx, vy, fcxb, fcyb);
 #pragma unroll
     for (int k = 0; k < kNv; ++k) {
-      double sx = solve_c[0 * kNv + k], sy = solve_c[1 * kNv + k];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        sx += p.guess_g[(0 * kNv + k) * 4 + j] * v[j];
-        sy += p.guess_g[(1 * kNv + k) * 4 + j] * v[4 + j];
-      }
-      fcxb[k] = float(sx);
-      fcyb[k] = float(sy);
       cxb[k] = double(fcxb[k]);
       cyb[k] = double(fcyb[k]);
     }
@@ -268,17 +286,13 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
 #pragma unroll
     for (int k = 0; k < kNv; ++k) liny[k] = liny[k] - tmp[k];
     // KKT solve: c = Kinv[:11,:11] (-lincost) + Kinv[:11,11:] b_eq
+    double nx[kNv], ny[kNv];
 #pragma unroll
-    for (int k = 0; k < kNv; ++k) {
-      double sx = solve_c[2 * kNv + k], sy = solve_c[3 * kNv + k];
-#pragma unroll
-      for (int j = 0; j < kNv; ++j) {
-        sx += p.proj_m[(0 * kNv + k) * kNv + j] * (-double(linx[j]));
-        sy += p.proj_m[(1 * kNv + k) * kNv + j] * (-double(liny[j]));
-      }
-      cx[k] = float(sx);
-      cy[k] = float(sy);
+    for (int j = 0; j < kNv; ++j) {
+      nx[j] = -double(linx[j]);
+      ny[j] = -double(liny[j]);
     }
+    gemv2_rows<kNv>(solve_c + 2 * kNv, solve_c + 3 * kNv, p.proj_m, p.proj_m + kNv * kNv, nx, ny, cx, cy);
   }
   double dcx[kNv], dcy[kNv];
 #pragma unroll
