@@ -26,7 +26,9 @@ import numpy as np
 from ._lib import native
 from .cem_helper import Helper
 
-_TOWN = {"Town10HD": "carla_town10hd", "Town10HD_Opt": "carla_town10hd"}
+# cem.py:161-166 tests town == "Town10HD" only: every other name, Town10HD_Opt
+# included, gets the Town05 lane bounds and desired lanes
+_TOWN = {"Town10HD": "carla_town10hd"}
 
 
 class CEM:

@@ -5,6 +5,7 @@
 
 #include <cmath>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 
@@ -80,12 +81,20 @@ FrenetState global_to_frenet(const PathView& p, float x, float y, float v, float
   return o;
 }
 
-const std::vector<double>& smoothing_inverse_cm(int P) {
+// The (P+1)^2 inverse, column-major.  Built outside the lock (O(P^3): a few
+// seconds at the 2048-point maximum), so other threads keep smoothing paths of
+// lengths already cached meanwhile; at most kCacheMax lengths are kept (the
+// reference uses one, num_path = 600), the oldest evicted first.  Callers hold
+// a shared_ptr, so an eviction never frees a matrix in use.
+std::shared_ptr<const std::vector<double>> smoothing_inverse_cm(int P) {
+  constexpr size_t kCacheMax = 4;
   static std::mutex mu;
-  static std::map<int, std::vector<double>> cache;
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = cache.find(P);
-  if (it != cache.end()) return it->second;
+  static std::vector<std::pair<int, std::shared_ptr<const std::vector<double>>>> cache;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    for (auto& e : cache)
+      if (e.first == P) return e.second;
+  }
   if (P < 4) throw std::invalid_argument("path smoothing needs >= 4 points");
   const int n = P + 1;
   // cost = 20 D3^T D3 + I (D3: third differences, (P-3) x P), KKT with e0
@@ -98,14 +107,20 @@ const std::vector<double>& smoothing_inverse_cm(int P) {
   a[size_t(P) * n + 0] = 1.0;
   a[size_t(0) * n + P] = 1.0;
   if (!invert(a, n)) throw std::runtime_error("singular path-smoothing KKT");
-  std::vector<double> cm(size_t(n) * n);
+  auto cm = std::make_shared<std::vector<double>>(size_t(n) * n);
   for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) cm[size_t(j) * n + i] = a[size_t(i) * n + j];
-  return cache.emplace(P, std::move(cm)).first->second;
+    for (int j = 0; j < n; ++j) (*cm)[size_t(j) * n + i] = a[size_t(i) * n + j];
+  std::lock_guard<std::mutex> lock(mu);
+  for (auto& e : cache)
+    if (e.first == P) return e.second;  // another thread built it meanwhile (the same bits)
+  if (cache.size() >= kCacheMax) cache.erase(cache.begin());
+  cache.emplace_back(P, cm);
+  return cm;
 }
 
 void path_smoothing(int P, const float* xw, const float* yw, float thr, float* xo, float* yo) {
-  const std::vector<double>& inv = smoothing_inverse_cm(P);
+  const auto inv_p = smoothing_inverse_cm(P);
+  const std::vector<double>& inv = *inv_p;
   const int n = P + 1;
   std::vector<float> alpha(P, 0.0f), d(P, thr), lx(P, 0.0f), ly(P, 0.0f), xs(xw, xw + P), ys(yw, yw + P);
   std::vector<double> rx(n), ry(n), sx(P), sy(P);

@@ -7,6 +7,7 @@
 // once; small dense products in fp64 (oracle/carla.py restates the same).
 #pragma once
 #include <cstdint>
+#include <memory>
 #include <vector>
 
 namespace mpcmmd {
@@ -32,8 +33,8 @@ FrenetState global_to_frenet(const PathView& path, float x, float y, float v, fl
 
 // inv([[20 D3^T D3 + I, e0^T], [e0, 0]]) for P path points
 // (C/opt/cem_helper.py:115-129), fp64 Gauss-Jordan, stored column-major
-// ((P+1) x (P+1)); cached per P.
-const std::vector<double>& smoothing_inverse_cm(int P);
+// ((P+1) x (P+1)); the last few P cached (built outside the cache lock).
+std::shared_ptr<const std::vector<double>> smoothing_inverse_cm(int P);
 
 // Helper.custom_path_smoothing (C/opt/cem_helper.py:279-318, 391-410).
 void path_smoothing(int P, const float* x_wp, const float* y_wp, float threshold, float* x_out, float* y_out);

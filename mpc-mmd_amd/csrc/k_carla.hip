@@ -141,8 +141,12 @@ __global__ __launch_bounds__(256) void k_risk_carla(Params p, int t, int mode) {
   }
   s1 = block_sum(s1, rs.d);
   s2 = block_sum(s2, rs.d);
-  // compute_lane_des_*: max(0, ||y - y1|| ||y - y2|| - gamma), one value for every row
-  const float cd = fmaxf(0.0f, float(sqrt(s1)) * float(sqrt(s2)) - p.gamma_des);
+  // compute_lane_des_*: max(0, ||y - y1|| ||y - y2|| - gamma), one value for every row.
+  // The two squared norms are fp64 sums rounded once (the reference: fp32
+  // jnp.linalg.norm; oracle/carla.py lane_des_bar does the same as here), and
+  // a NaN rollout gives NaN as jnp.maximum does (fmaxf would drop it)
+  const float cdv = float(sqrt(s1)) * float(sqrt(s2)) - p.gamma_des;
+  const float cd = cdv != cdv ? cdv : fmaxf(0.0f, cdv);
   for (int r = tid; r < S; r += blockDim.x) des[r] = cd;
   __syncthreads();
   float obs, lane, dl;

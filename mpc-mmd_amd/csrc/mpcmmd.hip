@@ -375,8 +375,16 @@ int ahead_kind(const mpcmmd_handle* h) {
 }
 
 // the Beta attempt table of iteration t, unless k_select of t - 1 drew it
+// (k_gamma_tab also zeroes the Beta fix-up count).  A table drawn ahead is
+// used once: ahead_t is cleared here, so a rerun of stage 2 / 4 for the same t
+// (stage API) draws the table again and restarts the fix-up list instead of
+// appending to it.
 void ensure_gamma_tab(mpcmmd_handle* h, int t) {
-  if (h->p.noise != MPCMMD_NOISE_BETA || h->ahead_t == t) return;
+  if (h->p.noise != MPCMMD_NOISE_BETA) return;
+  if (h->ahead_t == t) {
+    h->ahead_t = -1;  // consumed (this iteration's noise was drawn ahead too: stage 0 ran before)
+    return;
+  }
   h->launch(kKGammaTab, [&] { launch_gamma_tab(h->p, t, h->stream); });
   h->ahead_t = -1;  // the table's one slot now holds t
 }
@@ -1071,7 +1079,7 @@ int mpcmmd_iterate(mpcmmd_handle* h, int32_t t_begin, int32_t count) {
     } else {
       body(t_begin, count);
     }
-    h->last_t = t_begin + count - 1;
+    if (count > 0) h->last_t = t_begin + count - 1;  // a zero-count call runs nothing
     return MPCMMD_OK;
   });
 }

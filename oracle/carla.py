@@ -48,7 +48,9 @@ from .rng import STREAM_INIT_EPS, Draws, philox_normals
 
 F32 = np.float32
 F64 = np.float64
-TOWNS = {"Town05": "carla_town05", "Town10HD": "carla_town10hd", "Town10HD_Opt": "carla_town10hd"}
+# C/opt/cem.py:161-166: only the exact name "Town10HD" selects its constants
+# (Town10HD_Opt and any other town get Town05's)
+TOWNS = {"Town05": "carla_town05", "Town10HD": "carla_town10hd"}
 
 
 def f32(x):

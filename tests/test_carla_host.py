@@ -96,3 +96,21 @@ def test_replay_format_roundtrip(tmp_path):
     assert back["obstacles"].shape == (20, 8, 5) and np.all(back["obstacles"][:, :, 2:4] == 0)
     ob = R.nearest_obstacles(back["obstacles"][0], back["ego"][0], 3)
     assert ob.shape == (3, 5) and np.all(np.diff(np.hypot(ob[:, 0], ob[:, 1])) >= 0)
+
+
+def test_town_constants_follow_the_reference():
+    """C/opt/cem.py:161-166 tests ``town == "Town10HD"`` only; every other town
+    name (Town10HD_Opt, which main_carla.py:232 also accepts) gets the Town05
+    lane bounds and desired lanes.  The drop-in's mapping and the oracle's
+    agree with that."""
+    import importlib
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_gpu_carla import carla_package
+    mod = importlib.import_module(carla_package() + ".cem")
+    for town, want in (("Town05", "carla_town05"), ("Town10HD", "carla_town10hd"),
+                       ("Town10HD_Opt", "carla_town05"), ("Town03", "carla_town05")):
+        assert mod._TOWN.get(town, "carla_town05") == want
+        assert K.TOWNS.get(town, "carla_town05") == want
+    ora = K.CarlaCEM(4, 1, 3, 0.1, 30, "gaussian", "Town10HD_Opt", 0.0, 0.0, num_batch=20, maxiter_cem=1)
+    assert (ora.prob.y_lb, ora.prob.y_ub, ora.prob.y_des_2) == (-3.8, 0.3, -3.5)
