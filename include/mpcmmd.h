@@ -39,6 +39,10 @@ extern "C" {
 #define MPCMMD_COST_MMD_RANDOM 1
 #define MPCMMD_COST_CVAR 2
 #define MPCMMD_COST_SAA 3
+/* CARLA handles only: CEM.compute_cem_det of carla/optimizer/cem.py:633-790,
+ * the deterministic baseline -- one noisy initial state, the projection with
+ * its obstacle terms live (projection_det.py), no rollouts and no risk terms */
+#define MPCMMD_COST_DET 4
 
 /* noise models: Helper noise=="gaussian" / else beta (optimizer/cem_helper.py:405) */
 #define MPCMMD_NOISE_GAUSSIAN 0
@@ -198,7 +202,8 @@ typedef struct mpcmmd_path {
 } mpcmmd_path;
 
 /* CEM.compute_cem_mmd (cost_kind MPCMMD_COST_MMD_OPT) / compute_cem_cvar
- * (MPCMMD_COST_CVAR) of the CARLA optimizer (carla/optimizer/cem.py:217-629):
+ * (MPCMMD_COST_CVAR) / compute_cem_det (MPCMMD_COST_DET, num_obs <= 32) of
+ * the CARLA optimizer (carla/optimizer/cem.py:217-790):
  * init_state = init_state_global (x, y, v, vdot, psi, psidot), x_obs / y_obs
  * the Frenet obstacle tracks [O][100], path as above.  begin then
  * mpcmmd_iterate / mpcmmd_finish, or solve in one call.  out->steering,
@@ -278,7 +283,8 @@ int mpcmmd_run_stage(mpcmmd_handle* h, int32_t stage, int32_t t);
 /* Host-side batch-invariant constants (no GPU needed): fills dst with the
  * fp64 values of `name` ("P","Pdot","Pddot" [100][11] (fp32-rounded),
  * "P_prime" [H][11], "guess_kinv_x" [14][14], "guess_kinv_y" [15][15],
- * "proj_kinv_x", "proj_kinv_y", "fit" [11][H]).  Returns element count, or
+ * "proj_kinv_x", "proj_kinv_y", "fit" [11][H], "det_kinv_x", "det_kinv_y"
+ * (the CARLA det projection's, for cfg->num_obs obstacles)).  Returns element count, or
  * < 0 on error / when count is too small. */
 int mpcmmd_host_constant(const mpcmmd_config* cfg, const char* name, double* dst, size_t count);
 

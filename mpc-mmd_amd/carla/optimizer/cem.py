@@ -10,9 +10,10 @@ CEM of the CARLA experiments).  ``carla/main_carla.py`` does::
 
 With ``mpc-mmd_amd/carla`` on sys.path the same calls run on the MI355X
 through libmpcmmd.so (mpcmmd_carla_begin / iterate / finish; no JAX).
-``compute_cem_mmd`` and ``compute_cem_cvar`` are built; ``compute_cem_det``
-(the deterministic baseline with obstacle-constrained projection,
-projection_det.py) raises NotImplementedError.  Extra keyword-only options:
+``compute_cem_mmd``, ``compute_cem_cvar`` and ``compute_cem_det`` (the
+deterministic baseline with the obstacle-constrained projection of
+projection_det.py) are built, so every ``--costs`` of main_carla.py:188-194
+runs.  Extra keyword-only options:
 ``num_batch`` (reference: 100, cem.py:138), ``maxiter_cem``, ``device``,
 ``seed``; per call ``draws`` (explicit standard normals incl. ``init_eps``,
 include/mpcmmd.h) and ``trace``.
@@ -104,10 +105,14 @@ class CEM:
         return self._solve("cvar", idx_mpc, init_state_global, mean_param_init, cov_param_init, x_obs_traj,
                            y_obs_traj, v_des, x_path, y_path, arc_vec, Fx_dot, Fy_dot, kappa, **kw)
 
-    def compute_cem_det(self, *args, **kw):
-        """cem.py:633-790, the deterministic baseline (projection with active
-        obstacle terms, projection_det.py): not built."""
-        raise NotImplementedError("compute_cem_det (carla/optimizer/projection_det.py) is not built")
+    def compute_cem_det(self, idx_mpc, init_state_global, mean_param_init, cov_param_init, x_obs_traj, y_obs_traj,
+                        v_des, x_path, y_path, arc_vec, Fx_dot, Fy_dot, kappa, **kw):
+        """cem.py:633-790, the deterministic baseline: one noisy initial state
+        (cem_helper.py:680-696), the projection with its obstacle terms live
+        (projection_det.py), no rollouts and no risk terms ->
+        (cx_best, cy_best, v_best, steering_best, mean_param)."""
+        return self._solve("det", idx_mpc, init_state_global, mean_param_init, cov_param_init, x_obs_traj,
+                           y_obs_traj, v_des, x_path, y_path, arc_vec, Fx_dot, Fy_dot, kappa, **kw)
 
     @property
     def handle(self):

@@ -229,6 +229,44 @@ ProblemConsts build_constants(int num_prime, int variant) {
   return c;
 }
 
+void det_projection_kinv(const ProblemConsts& c, int num_obs, std::vector<double>& kx, std::vector<double>& ky) {
+  if (num_obs < 1) throw std::runtime_error("det projection: num_obs >= 1");
+  const std::vector<double>& P = c.P;
+  auto a = atb(c.Pdd.data(), c.Pdd.data(), kNum, kNvar, kNvar);
+  auto b = atb(c.Pd.data(), c.Pd.data(), kNum, kNvar, kNvar);
+  std::vector<double> base(kNvar * kNvar);
+  for (int i = 0; i < kNvar; ++i)
+    for (int j = 0; j < kNvar; ++j) base[i * kNvar + j] = (i == j ? 1.0 : 0.0) + a[i * kNvar + j] + b[i * kNvar + j];
+  std::vector<double> Al(size_t(kLane) * kNvar);
+  for (int r = 0; r < kNum - 1; ++r)
+    for (int j = 0; j < kNvar; ++j) {
+      Al[r * kNvar + j] = P[(r + 1) * kNvar + j];
+      Al[(r + kNum - 1) * kNvar + j] = -P[(r + 1) * kNvar + j];
+    }
+  auto ll = atb(Al.data(), Al.data(), kLane, kNvar, kNvar);
+  // A_obs = tile(P, (num_obs, 1)) (carla/optimizer/cem.py:66), accumulated row by row
+  std::vector<double> Ao(size_t(num_obs) * kNum * kNvar);
+  for (int o = 0; o < num_obs; ++o)
+    for (int i = 0; i < kNum * kNvar; ++i) Ao[size_t(o) * kNum * kNvar + i] = P[i];
+  auto oo = atb(Ao.data(), Ao.data(), num_obs * kNum, kNvar, kNvar);
+  std::vector<double> cx(base), cy(base);
+  for (int i = 0; i < kNvar * kNvar; ++i) {
+    cx[i] += oo[i];
+    cy[i] += ll[i];
+    cy[i] += oo[i];
+  }
+  std::vector<double> Aeq_x(3 * kNvar), Aeq_y(4 * kNvar);
+  for (int j = 0; j < kNvar; ++j) {
+    Aeq_x[0 * kNvar + j] = Aeq_y[0 * kNvar + j] = P[j];
+    Aeq_x[1 * kNvar + j] = Aeq_y[1 * kNvar + j] = c.Pd[j];
+    Aeq_x[2 * kNvar + j] = Aeq_y[2 * kNvar + j] = c.Pdd[j];
+    Aeq_y[3 * kNvar + j] = c.Pd[(kNum - 1) * kNvar + j];
+  }
+  kx = kkt(cx, Aeq_x, 3);
+  ky = kkt(cy, Aeq_y, 4);
+  if (!invert(kx, 14) || !invert(ky, 15)) throw std::runtime_error("singular det projection KKT");
+}
+
 DynObsConsts build_dyn_obs_consts() {
   // obs_data.__init__ (obs_data_generate_dynamic.py:10-36): the same
   // linspace(0, 15, 100) basis, cast to fp32 by jnp.asarray

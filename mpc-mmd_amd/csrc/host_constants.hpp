@@ -68,6 +68,12 @@ void dyn_obs_traj(const DynObsConsts& c, int num_obs, const float* x0, const flo
 // matrix (never for valid H >= 2).
 ProblemConsts build_constants(int num_prime, int variant);
 
+// KKT inverses of the CARLA det projection (carla/optimizer/projection_det.py:
+// 149-160): the projection KKT cost matrices plus rho_obs A_obs^T A_obs, A_obs
+// = tile(P, (num_obs, 1)) accumulated row by row (oracle/problem.py: det_kinv
+// in the same order).  kx [14][14], ky [15][15].
+void det_projection_kinv(const ProblemConsts& c, int num_obs, std::vector<double>& kx, std::vector<double>& ky);
+
 // numpy.linspace(start, stop, num) (fp64, endpoint included).
 std::vector<double> linspace(double start, double stop, int num);
 

@@ -8,6 +8,13 @@
 //     compute_alph_d       :193-274
 //   compute_controls     optimizer/cem_helper.py:540-551
 //
+// k_front<true> is compute_cem_det's projection (carla/optimizer/
+// projection_det.py:56-336): the same, plus the obstacle terms the other
+// projections leave dead -- per (obstacle, point) polar forms alpha_obs /
+// d_obs on the guess and on the projected trajectory, rho_obs A_obs^T b_obs in
+// the linear cost, its own KKT inverse (A_obs^T A_obs in the cost), the
+// obstacle residual in res_norm and A_obs^T r_obs in the multipliers.
+//
 // Lane l owns planning points t = l and t = l + 64 (< 100).  The 100x11
 // Bernstein bases are staged once per workgroup in LDS (13.2 KB).  Every
 // basis product P c / P^T r accumulates in fp64 and is rounded to fp32 where
@@ -112,6 +119,30 @@ struct Polar {
   float ca, sa, d;
 };
 
+// the det projection's obstacle polar form (projection_det.py:69-73,
+// 210-214) of the offset (wc, ws) = (x - x_obs, y - y_obs):
+// alpha = atan2(ws a, wc b), d = (a wc cos + b ws sin) / (a^2 cos^2 + b^2 sin^2)
+DEVI Polar obs_polar(float wc, float ws, const Params& p) {
+  const float al = cr_atan2(ws * p.obs_a, wc * p.obs_b);
+  const float ca = cr_cos(al), sa = cr_sin(al);
+  const float c1 = p.obs_a2 * (ca * ca) + p.obs_b2 * (sa * sa);
+  const float c2 = (p.obs_a * wc) * ca + (p.obs_b * ws) * sa;
+  return Polar{ca, sa, c2 / c1};
+}
+
+// jnp.maximum(lo, v), NaN propagating
+DEVI float max_nan(float lo, float v) { return v != v ? v : fmaxf(lo, v); }
+
+DEVI unsigned long long readlane_u64(unsigned long long v, int l) {
+  const unsigned lo = __builtin_amdgcn_readlane(int(unsigned(v)), l), hi = __builtin_amdgcn_readlane(int(unsigned(v >> 32)), l);
+  return (unsigned long long)hi << 32 | lo;
+}
+
+DEVI unsigned long long shfl_up_u64(unsigned long long v, int d) {
+  const int lo = __shfl_up(int(unsigned(v)), d, kWave), hi = __shfl_up(int(unsigned(v >> 32)), d, kWave);
+  return (unsigned long long)unsigned(hi) << 32 | unsigned(lo);
+}
+
 // alpha = atan2(wy, wx); d = clip((wx cos + wy sin) / (cos^2 + sin^2), lo, hi)
 DEVI Polar polar_of(float alpha, float wx, float wy, float lo, float hi) {
   const float ca = cr_cos(alpha), sa = cr_sin(alpha);
@@ -144,17 +175,25 @@ DEVI void gemv2_rows(const double* cx0, const double* cy0, const double* Ax, con
   }
 }
 
+template <bool kDet>
 __global__ __launch_bounds__(256) void k_front(Params p, int t) {
   __shared__ float sB[3 * kN * kNv];
-  extern __shared__ float sPath[];  // CARLA: arc_vec [P], kappa [P] of the candidate block's configuration
+  // CARLA: arc_vec [P], kappa [P] of the candidate block's configuration;
+  // det: then its obstacle tracks x_obs [O][100], y_obs [O][100]
+  extern __shared__ float sPath[];
   for (int i = threadIdx.x; i < 3 * kN * kNv; i += blockDim.x) sB[i] = p.basis[i];
   if (p.carla) {
     // every candidate of a block belongs to one configuration when B % 4 == 0
     // (the host checks); the block's first candidate names it
-    const float* pa = p.path + size_t(min(blockIdx.x * 4, p.Bt - 1) / p.B) * 6 * kMaxPath;
+    const int g = min(blockIdx.x * 4, p.Bt - 1) / p.B;
+    const float* pa = p.path + size_t(g) * 6 * kMaxPath;
     for (int i = threadIdx.x; i < p.P; i += blockDim.x) {
       sPath[i] = pa[2 * kMaxPath + i];
       sPath[p.P + i] = pa[5 * kMaxPath + i];
+    }
+    if (kDet) {
+      const float* of = p.obs_full + size_t(g) * 2 * p.O * kN;
+      for (int i = threadIdx.x; i < 2 * p.O * kN; i += blockDim.x) sPath[2 * p.P + i] = of[i];
     }
   }
   __syncthreads();
@@ -239,6 +278,45 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
     for (int k = 0; k < kNv; ++k) ly[k] = (ly[k] - tmp[k]) - tmp2[k];
   }
 
+  // ---- det: obstacle polar forms on the guess (projection_det.py:60-74) and
+  // rho_obs A_obs^T b_obs of compute_x (:143-147, 164, 169); the multipliers
+  // get no obstacle term here (:119-123).  sobs_* = A_obs^T b_obs_* (fp64)
+  const float* xob = sPath + 2 * p.P;
+  const float* yob = xob + p.O * kN;
+  float obsx[kNv], obsy[kNv];
+  unsigned long long nonfin = 0;  // bit 2 o + q: d_obs of the guess at (o, point q) is not finite
+  if (kDet) {
+    double sox[kNv], soy[kNv];
+#pragma unroll
+    for (int k = 0; k < kNv; ++k) sox[k] = soy[k] = 0.0;
+    float xg[2], yg[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      xg[q] = eval_row(R.P[q], cxb);
+      yg[q] = eval_row(R.P[q], cyb);
+    }
+    for (int o = 0; o < p.O; ++o) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (q == 1 && !v1) continue;
+        const int tt = q == 0 ? t0 : t1;
+        const float xo = xob[o * kN + tt], yo = yob[o * kN + tt];
+        const Polar op = obs_polar(xg[q] - xo, yg[q] - yo, p);
+        const float d0 = max_nan(1.0f, op.d);
+        if (!isfinite(d0)) nonfin |= 1ull << (2 * o + q);
+        const float bx = xo + (d0 * op.ca) * p.obs_a;  // x_obs + d cos(alpha) a
+        const float by = yo + (d0 * op.sa) * p.obs_b;
+#pragma unroll
+        for (int k = 0; k < kNv; ++k) {
+          sox[k] += double(R.P[q][k]) * double(bx);
+          soy[k] += double(R.P[q][k]) * double(by);
+        }
+      }
+    }
+    totals11(sox, obsx);
+    totals11(soy, obsy);
+  }
+
   MPCMMD_STAMP(p, 43);
   // ---- compute_x (projection.py:123-185) --------------------------------------
   // lane-bound rows j = t-1 (t = 1..99): ub row j, lb row 99 + j; A_lane = [P[1:]; -P[1:]]
@@ -269,6 +347,9 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
     adj(R.D[0], vxb[0], R.D[1], vxb[1], v1, tmp2);
 #pragma unroll
     for (int k = 0; k < kNv; ++k) linx[k] = ((-lx[k] - fcxb[k]) - tmp[k]) - tmp2[k];
+    if (kDet)
+#pragma unroll
+      for (int k = 0; k < kNv; ++k) linx[k] = linx[k] - obsx[k];
     adj(R.DD[0], by[0], R.DD[1], by[1], v1, tmp);
     adj(R.D[0], vyb[0], R.D[1], vyb[1], v1, tmp2);
 #pragma unroll
@@ -285,6 +366,9 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
     totals11(sa, tmp);
 #pragma unroll
     for (int k = 0; k < kNv; ++k) liny[k] = liny[k] - tmp[k];
+    if (kDet)
+#pragma unroll
+      for (int k = 0; k < kNv; ++k) liny[k] = liny[k] - obsy[k];
     // KKT solve: c = Kinv[:11,:11] (-lincost) + Kinv[:11,11:] b_eq
     double nx[kNv], ny[kNv];
 #pragma unroll
@@ -292,7 +376,8 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
       nx[j] = -double(linx[j]);
       ny[j] = -double(liny[j]);
     }
-    gemv2_rows<kNv>(solve_c + 2 * kNv, solve_c + 3 * kNv, p.proj_m, p.proj_m + kNv * kNv, nx, ny, cx, cy);
+    const double* pm = kDet ? p.proj_m_det : p.proj_m;
+    gemv2_rows<kNv>(solve_c + 2 * kNv, solve_c + 3 * kNv, pm, pm + kNv * kNv, nx, ny, cx, cy);
   }
   double dcx[kNv], dcy[kNv];
 #pragma unroll
@@ -352,18 +437,59 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
       n_lane += double(rl_ub[q]) * double(rl_ub[q]) + double(rl_lb[q]) * double(rl_lb[q]);
     }
   }
+  // ---- det: obstacle residuals on the projected trajectory (projection_det.py:
+  // 201-217, 257-274): d_obs >= 1 + (1 - gamma_obs) (d_obs_prev - 1), the
+  // previous d_obs shifted one point (comp_d_obs_prev, :192-195; gamma_obs = 1,
+  // so the bound is 1, or NaN where the shifted guess value is not finite)
+  double n_obs = 0.0;
+  float rox[kNv], roy[kNv];
+  if (kDet) {
+    constexpr unsigned long long kEven = 0x5555555555555555ull;
+    const unsigned long long up = shfl_up_u64(nonfin, 1), m63 = readlane_u64(nonfin, 63);
+    const unsigned long long prev0 = lane == 0 ? 0ull : (up & kEven);           // point t0 - 1 (t0 = 0: the 1)
+    const unsigned long long prev1 = lane == 0 ? (m63 & kEven) : ((up >> 1) & kEven);  // point t1 - 1
+    double sx[kNv], sy[kNv];
+#pragma unroll
+    for (int k = 0; k < kNv; ++k) sx[k] = sy[k] = 0.0;
+    const float qnan = __int_as_float(0x7fc00000);
+    for (int o = 0; o < p.O; ++o) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (q == 1 && !v1) continue;
+        const int tt = q == 0 ? t0 : t1;
+        const float wc = x[q] - xob[o * kN + tt], ws = y[q] - yob[o * kN + tt];
+        const Polar op = obs_polar(wc, ws, p);
+        const bool pnf = (((q == 0 ? prev0 : prev1) >> (2 * o)) & 1ull) != 0;
+        const float d = pnf ? qnan : max_nan(1.0f, op.d);
+        const float rx = wc - (p.obs_a * d) * op.ca, ry = ws - (p.obs_b * d) * op.sa;
+        n_obs += double(rx) * double(rx) + double(ry) * double(ry);
+#pragma unroll
+        for (int k = 0; k < kNv; ++k) {
+          sx[k] += double(R.P[q][k]) * double(rx);
+          sy[k] += double(R.P[q][k]) * double(ry);
+        }
+      }
+    }
+    totals11(sx, rox);
+    totals11(sy, roy);
+  }
   {
-    const double nv[3] = {n_acc, n_vel, n_lane};
+    const double nv[4] = {n_acc, n_vel, n_lane, n_obs};
     const double z = wave_totals16_d(nv);
     n_acc = readlane_d(z, 0);
     n_vel = readlane_d(z, 4);
     n_lane = readlane_d(z, 8);
+    n_obs = readlane_d(z, 12);
   }
-  const float rn = (float(sqrt(n_acc)) + float(sqrt(n_vel))) + float(sqrt(n_lane));
+  float rn = (float(sqrt(n_acc)) + float(sqrt(n_vel))) + float(sqrt(n_lane));
+  if (kDet) rn = rn + float(sqrt(n_obs));
   adj(R.DD[0], rax[0], R.DD[1], rax[1], v1, tmp);
   adj(R.D[0], rvx[0], R.D[1], rvx[1], v1, tmp2);
 #pragma unroll
   for (int k = 0; k < kNv; ++k) lx[k] = (lx[k] - tmp[k]) - tmp2[k];
+  if (kDet)
+#pragma unroll
+    for (int k = 0; k < kNv; ++k) lx[k] = lx[k] - rox[k];
   adj(R.DD[0], ray[0], R.DD[1], ray[1], v1, tmp);
   adj(R.D[0], rvy[0], R.D[1], rvy[1], v1, tmp2);
   {
@@ -379,6 +505,9 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
     totals11(sa, t3);
 #pragma unroll
     for (int k = 0; k < kNv; ++k) ly[k] = ((ly[k] - tmp[k]) - tmp2[k]) - t3[k];
+    if (kDet)
+#pragma unroll
+      for (int k = 0; k < kNv; ++k) ly[k] = ly[k] - roy[k];
   }
 
   MPCMMD_STAMP(p, 45);
@@ -462,7 +591,12 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
 }  // namespace
 
 void launch_front(const Params& p, int t, hipStream_t s) {
-  hipLaunchKernelGGL(k_front, dim3((p.Bt + 3) / 4), dim3(256), p.carla ? size_t(2) * p.P * 4 : 0, s, p, t);
+  if (p.cost == 4) {  // MPCMMD_COST_DET (CARLA handles only)
+    const size_t lds = (size_t(2) * p.P + size_t(2) * p.O * kN) * 4;
+    hipLaunchKernelGGL(k_front<true>, dim3((p.Bt + 3) / 4), dim3(256), lds, s, p, t);
+    return;
+  }
+  hipLaunchKernelGGL(k_front<false>, dim3((p.Bt + 3) / 4), dim3(256), p.carla ? size_t(2) * p.P * 4 : 0, s, p, t);
 }
 
 }  // namespace mpcmmd

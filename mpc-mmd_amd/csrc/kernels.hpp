@@ -59,6 +59,7 @@ constexpr int kMomStride = 16;
 constexpr int kMomR = 12;
 constexpr int kMaxSplit = 8;  // workgroups per candidate of the row-sum kernels
 constexpr int kMaxPath = 2048;  // CARLA path points (the reference's num_path = 600)
+constexpr int kMaxDetObs = 32;  // obstacles of compute_cem_det (k_front's per-lane non-finite mask: 2 bits each)
 
 struct Params {
   // shapes / configuration.  A launch covers G configurations of B
@@ -165,6 +166,7 @@ struct Params {
   int32_t R0;              // noisy initial rows per configuration (n^2 mmd_opt, n cvar)
   float wheel_base;        // carla/optimizer/cem.py:27
   float obs_a2, obs_b2;    // a_obs^2, b_obs^2 (cem.py:26)
+  float obs_a, obs_b;      // a_obs, b_obs (the det projection's obstacle polar forms)
   float a_centr;           // cem.py:29
   float y_des1, y_des2;    // cem.py:161-166
   float w_des;             // weight of the desired-lane risk (cem.py:171-173)
@@ -175,6 +177,10 @@ struct Params {
   float* lane_des;         // [Bt] desired-lane risk (costs.py:70-100), unweighted
   float* rxy;              // [Bt][S][2][H] rollout points: global (x, y), then Frenet (s, d) in place
   float* res_steer;        // [G][T][100] steering of each iteration's chosen elite
+  // compute_cem_det (cost MPCMMD_COST_DET): the projection with its obstacle
+  // terms live (carla/optimizer/projection_det.py)
+  const double* proj_m_det;  // [2][11][11] Kinv[:11,:11] of the det KKT (x, y)
+  const float* obs_full;     // [G][2][O][100] Frenet obstacle tracks, all 100 plan points
   // outputs
   float* results;          // [G][T][kResultStride]
   int32_t* tr_proj;        // [G][T][B]

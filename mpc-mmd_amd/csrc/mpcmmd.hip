@@ -99,6 +99,7 @@ struct mpcmmd_handle {
   bool mmd_ok = false;                // mmd_opt buffers allocated (mmdopt_supported)
   bool carla = false;                 // CARLA variant handle (mpcmmd_carla_begin)
   int R0 = 0;                         // noisy initial rows per configuration (CARLA)
+  std::vector<double> det_kx, det_ky;  // KKT inverses of the CARLA det projection (14^2, 15^2)
   std::string mmd_why;
   // pinned staging for the per-solve uploads of mpcmmd_begin: the copies are
   // asynchronous, so their source must outlive the call; the next begin waits
@@ -371,7 +372,8 @@ void run_carla_risk(mpcmmd_handle* h, int t, int mode) {
 // the draws k_select produces ahead for this solve (mpcmmd_handle::ahead_t)
 int ahead_kind(const mpcmmd_handle* h) {
   if (!h->ahead_on) return 0;
-  return (h->ext_roll && h->ext_res ? 0 : kAheadNoise) | (h->p.noise == MPCMMD_NOISE_BETA ? kAheadGamma : 0);
+  const bool beta = h->p.noise == MPCMMD_NOISE_BETA && h->p.cost != MPCMMD_COST_DET;  // det: no rollouts
+  return (h->ext_roll && h->ext_res ? 0 : kAheadNoise) | (beta ? kAheadGamma : 0);
 }
 
 // the Beta attempt table of iteration t, unless k_select of t - 1 drew it
@@ -399,6 +401,7 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
       h->launch(kKFront, [&] { launch_front(p, t, h->stream); });
       break;
     case 2:
+      if (p.cost == MPCMMD_COST_DET) break;  // compute_cem_det: no rollouts, zero risks (carla/optimizer/cem.py:717-722)
       ensure_gamma_tab(h, t);
       if (p.cost == MPCMMD_COST_MMD_OPT) {
         if (!h->mmd_ok) throw std::invalid_argument("mmd_opt unsupported for this configuration: " + h->mmd_why);
@@ -566,6 +569,8 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     p.wheel_base = float(h->pc.wheel_base);
     p.obs_a2 = float(h->pc.a_obs * h->pc.a_obs);
     p.obs_b2 = float(h->pc.b_obs * h->pc.b_obs);
+    p.obs_a = float(h->pc.a_obs);
+    p.obs_b = float(h->pc.b_obs);
     p.a_centr = float(h->pc.a_centr);
     p.y_des1 = float(h->pc.y_des_1);
     p.y_des2 = float(h->pc.y_des_2);
@@ -647,8 +652,20 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
       p.bkred = (float*)h->alloc("bkred", BT * kBetaSamples * tri_stride(int(n)) * 4);
       p.ygen = (float*)h->alloc("ygen", BT * kBzCols * ygen_stride(h->M) * 4);
     }
+    std::vector<double> pm_det;
     if (h->carla) {  // path, noisy initial rows, curvature, rollout points, steering results
       h->R0 = mmd_ok ? std::max(h->M, S) : S;
+      // compute_cem_det's projection (projection_det.py:149-160): its own KKT
+      det_projection_kinv(h->pc, O, h->det_kx, h->det_ky);
+      pm_det.assign(2 * kNvar * kNvar, 0.0);
+      for (int xy = 0; xy < 2; ++xy) {
+        const auto& Ki = xy == 0 ? h->det_kx : h->det_ky;
+        const int n = xy == 0 ? 14 : 15;
+        for (int k = 0; k < kNvar; ++k)
+          for (int j = 0; j < kNvar; ++j) pm_det[(xy * kNvar + k) * kNvar + j] = Ki[k * n + j];
+      }
+      p.proj_m_det = (const double*)h->alloc("proj_m_det", pm_det.size() * 8);
+      p.obs_full = (const float*)h->alloc("obs_full", size_t(GM) * 2 * O * kNum * 4);
       p.R0 = h->R0;
       p.path = (const float*)h->alloc("path", size_t(GM) * 6 * kMaxPath * 4);
       p.st0r = (const float*)h->alloc("st0r", size_t(GM) * h->R0 * 8 * 4);
@@ -702,13 +719,15 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
         HIPC(hipEventCreateWithFlags(&h->gev_done[g], hipEventDisableTiming));
       }
     }
-    h->stage_bytes = stage_size(B, S, H, O, T, GM) + (h->carla ? size_t(6) * kMaxPath * 4 + size_t(h->R0) * 8 * 4 + 256 : 0);
+    h->stage_bytes = stage_size(B, S, H, O, T, GM) +
+                     (h->carla ? size_t(6) * kMaxPath * 4 + size_t(h->R0) * 8 * 4 + size_t(2) * O * kNum * 4 + 512 : 0);
     HIPC(hipHostMalloc(reinterpret_cast<void**>(&h->stage), h->stage_bytes, hipHostMallocDefault));
     HIPC(hipEventCreateWithFlags(&h->stage_ev, hipEventDisableTiming));
     upload(h, "basis", basis.data(), basis.size() * 4);
     upload(h, "guess_g", gg.data(), gg.size() * 8);
     upload(h, "proj_m", pm.data(), pm.size() * 8);
     upload(h, "fit", h->pc.fit.data(), h->pc.fit.size() * 8);
+    if (h->carla) upload(h, "proj_m_det", pm_det.data(), pm_det.size() * 8);
     HIPC(hipStreamSynchronize(h->stream));
     return MPCMMD_OK;
   });
@@ -776,7 +795,8 @@ namespace {
 // init_state_global = (x, y, v, vdot, psi, psidot) (C/main_carla.py:352).
 void carla_rows(mpcmmd_handle* h, int cost_kind, int32_t idx_mpc, const float* is, const mpcmmd_path& path,
                 const mpcmmd_draws* draws, std::vector<float>& rows, double* bx, double* by) {
-  const int R = cost_kind == MPCMMD_COST_MMD_OPT ? h->M : h->S;
+  // compute_noisy_init_state / _baseline / _det (cem_helper.py:661-715): n^2, n or 1 rows
+  const int R = cost_kind == MPCMMD_COST_MMD_OPT ? h->M : cost_kind == MPCMMD_COST_DET ? 1 : h->S;
   std::vector<float> eps;
   if (draws && draws->init_eps) eps.assign(draws->init_eps, draws->init_eps + size_t(R) * 4);
   else eps = host_normals(uint32_t(idx_mpc), h->cfg.seed, kStreamInitEps, 0, size_t(R) * 4);
@@ -818,12 +838,17 @@ int begin_impl(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t
   if (h->carla != (path != nullptr))
     return fail(MPCMMD_E_INVALID, h->carla ? "CARLA handle: use mpcmmd_carla_begin / mpcmmd_carla_solve (a path is needed)"
                                            : "mpcmmd_carla_begin needs a handle of a CARLA variant");
-  if (h->carla && cost_kind != MPCMMD_COST_MMD_OPT && cost_kind != MPCMMD_COST_CVAR)
-    return fail(MPCMMD_E_UNSUPPORTED, "the CARLA optimizer has compute_cem_mmd (mmd_opt) and compute_cem_cvar only");
+  if (h->carla && cost_kind != MPCMMD_COST_MMD_OPT && cost_kind != MPCMMD_COST_CVAR && cost_kind != MPCMMD_COST_DET)
+    return fail(MPCMMD_E_UNSUPPORTED,
+                "the CARLA optimizer has compute_cem_mmd (mmd_opt), compute_cem_cvar and compute_cem_det only");
+  if (!h->carla && cost_kind == MPCMMD_COST_DET)
+    return fail(MPCMMD_E_INVALID, "compute_cem_det exists for the CARLA optimizer only");
+  if (cost_kind == MPCMMD_COST_DET && h->O > kMaxDetObs)
+    return fail(MPCMMD_E_UNSUPPORTED, "compute_cem_det: num_obs <= 32");
   if (path && (path->num_path < 4 || path->num_path > kMaxPath || !path->x_path || !path->y_path || !path->arc_vec ||
                !path->Fx_dot || !path->Fy_dot || !path->kappa))
     return fail(MPCMMD_E_INVALID, "path: 4 <= num_path <= 2048 and six arrays");
-  if (cost_kind < 0 || cost_kind > 3) return fail(MPCMMD_E_INVALID, "cost_kind must be 0..3");
+  if (cost_kind < 0 || cost_kind > 4) return fail(MPCMMD_E_INVALID, "cost_kind must be 0..4");
   if (n_cfg < 1 || n_cfg > h->Gmax) return fail(MPCMMD_E_INVALID, "n_cfg must be 1..max_configs of the handle");
   if (draws && n_cfg > 1) return fail(MPCMMD_E_INVALID, "external draws need n_cfg == 1");
   if (cost_kind == MPCMMD_COST_MMD_OPT && !h->mmd_ok) return fail(MPCMMD_E_UNSUPPORTED, h->mmd_why);
@@ -850,13 +875,13 @@ int begin_impl(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t
     p.b0 = 0;
     p.nb = p.Bt;
     // cem.py:161-163 weights (obs, lane); CARLA: carla/optimizer/cem.py:171-173 (+ desired lane)
-    const float w_obs[4] = {1e3f, 1e3f, 1e3f, 1e6f}, w_lane[4] = {0.f, 0.f, 0.f, 1e6f};
+    const float w_obs[5] = {1e3f, 1e3f, 1e3f, 1e6f, 0.f}, w_lane[5] = {0.f, 0.f, 0.f, 1e6f, 0.f};
     p.w_obs = w_obs[cost_kind];
     p.w_lane = w_lane[cost_kind];
     p.w_des = 0.0f;
-    if (h->carla) {
-      p.w_obs = cost_kind == MPCMMD_COST_MMD_OPT ? 0.1f : 100.0f;
-      p.w_lane = cost_kind == MPCMMD_COST_MMD_OPT ? 0.01f : 25.0f;
+    if (h->carla) {  // det: 0 * the zero risks (cem.py:750)
+      p.w_obs = cost_kind == MPCMMD_COST_MMD_OPT ? 0.1f : cost_kind == MPCMMD_COST_DET ? 0.0f : 100.0f;
+      p.w_lane = cost_kind == MPCMMD_COST_MMD_OPT ? 0.01f : cost_kind == MPCMMD_COST_DET ? 0.0f : 25.0f;
       p.w_des = 0.0f;
     }
     upload_staged(h, "idx_mpc", idx_mpc, size_t(G) * 4);
@@ -878,8 +903,11 @@ int begin_impl(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t
       for (int k = 0; k < kNvar; ++k) {
         for (int e = 0; e < 3; ++e) scg[0 * kNvar + k] += h->pc.guess_kinv_x[k * 14 + kNvar + e] * bx[e];
         for (int e = 0; e < 4; ++e) scg[1 * kNvar + k] += h->pc.guess_kinv_y[k * 15 + kNvar + e] * by[e];
-        for (int e = 0; e < 3; ++e) scg[2 * kNvar + k] += h->pc.proj_kinv_x[k * 14 + kNvar + e] * bx[e];
-        for (int e = 0; e < 4; ++e) scg[3 * kNvar + k] += h->pc.proj_kinv_y[k * 15 + kNvar + e] * by[e];
+        const bool det = cost_kind == MPCMMD_COST_DET;  // the det projection's own KKT
+        const double* pkx = det ? h->det_kx.data() : h->pc.proj_kinv_x.data();
+        const double* pky = det ? h->det_ky.data() : h->pc.proj_kinv_y.data();
+        for (int e = 0; e < 3; ++e) scg[2 * kNvar + k] += pkx[k * 14 + kNvar + e] * bx[e];
+        for (int e = 0; e < 4; ++e) scg[3 * kNvar + k] += pky[k * 15 + kNvar + e] * by[e];
       }
       float* s0 = st0.data() + size_t(g) * 8;
       s0[0] = is[0], s0[1] = is[1], s0[2] = is[2], s0[3] = is[3], s0[4] = atan2f(is[3], is[2]);
@@ -912,6 +940,13 @@ int begin_impl(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t
       for (int k = 0; k < 6; ++k)
         upload_staged(h, "path", arrs[k], size_t(path->num_path) * 4, size_t(k) * kMaxPath * 4);
       p.P = path->num_path;
+      if (cost_kind == MPCMMD_COST_DET) {  // all 100 plan points of the tracks; risks stay 0 (no risk stage)
+        upload_staged(h, "obs_full", x_obs, size_t(O) * kNum * 4);
+        upload_staged(h, "obs_full", y_obs, size_t(O) * kNum * 4, size_t(O) * kNum * 4);
+        HIPC(hipMemsetAsync(p.obs_cost, 0, size_t(B) * 4, h->stream));
+        HIPC(hipMemsetAsync(p.lane_cost, 0, size_t(B) * 4, h->stream));
+        HIPC(hipMemsetAsync(p.lane_des, 0, size_t(B) * 4, h->stream));
+      }
     }
     upload_staged(h, "st0", st0.data(), st0.size() * 4);
     upload_staged(h, "obs", ob.data(), ob.size() * 4);
@@ -1305,7 +1340,12 @@ int mpcmmd_host_constant(const mpcmmd_config* cfg, const char* name, double* dst
     else if (n == "proj_kinv_x") v = &c.proj_kinv_x;
     else if (n == "proj_kinv_y") v = &c.proj_kinv_y;
     else if (n == "fit") v = &c.fit;
-    else return fail(MPCMMD_E_INVALID, "unknown constant " + n);
+    std::vector<double> dk[2];
+    if (n == "det_kinv_x" || n == "det_kinv_y") {
+      det_projection_kinv(c, cfg->num_obs, dk[0], dk[1]);
+      v = &dk[n == "det_kinv_y" ? 1 : 0];
+    }
+    if (!v) return fail(MPCMMD_E_INVALID, "unknown constant " + n);
     if (dst) {
       if (count < v->size()) return fail(MPCMMD_E_INVALID, "dst too small");
       std::memcpy(dst, v->data(), v->size() * 8);

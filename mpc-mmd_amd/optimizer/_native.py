@@ -14,7 +14,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MPCMMD_LIB", os.path.join(os.path.dirname(_HERE), "libmpcmmd.so"))
 
-COST = {"mmd_opt": 0, "mmd_random": 1, "cvar": 2, "saa": 3}
+COST = {"mmd_opt": 0, "mmd_random": 1, "cvar": 2, "saa": 3, "det": 4}  # det: CARLA handles (compute_cem_det)
 NOISE = {"gaussian": 0, "beta": 1}
 VARIANT = {"static": 0, "dynamic": 1, "carla_town05": 2, "carla_town10hd": 3}
 RESULT_STRIDE_BETA_MAX = 32
@@ -302,8 +302,9 @@ class Handle:
                                    _fptr(ins["y_obs"]), float(v_des), None if d is None else C.byref(d)))
 
     def carla_begin(self, cost, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des, path, draws=None):
-        """mpcmmd_carla_begin: compute_cem_mmd / compute_cem_cvar of the CARLA
-        optimizer (carla/optimizer/cem.py:217-629); path: dict of PATH_KEYS."""
+        """mpcmmd_carla_begin: compute_cem_mmd / compute_cem_cvar / compute_cem_det
+        of the CARLA optimizer (carla/optimizer/cem.py:217-790; cost "mmd_opt",
+        "cvar", "det"); path: dict of PATH_KEYS."""
         ins = self._inputs(init_state, mean, cov, x_obs, y_obs, draws)
         pth, keep = make_path(path)
         ins["_path"] = (pth, keep)

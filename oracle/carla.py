@@ -380,8 +380,10 @@ class CarlaCEM(CEM):
 
     # -- per-solve setup (C/opt/cem.py:248-264, 476-492) -------------------
     def rows(self, cost):
+        """Noisy initial states: n^2 (compute_noisy_init_state), n (_baseline)
+        or 1 (_det) (C/opt/cem_helper.py:661-715)."""
         p = self.prob
-        return p.num_reduced ** 2 if cost == "mmd_opt" else p.num_reduced
+        return {"mmd_opt": p.num_reduced ** 2, "det": 1}.get(cost, p.num_reduced)
 
     def noisy_init(self, init_state, eps):
         """compute_noisy_init_state(_baseline) (C/opt/cem_helper.py:660-715):
@@ -424,13 +426,19 @@ class CarlaCEM(CEM):
         return st
 
     # -- per iteration ------------------------------------------------------
-    def front_carla(self, st, path):
+    def front_carla(self, st, path, det_obs=None):
         """compute_x_guess + the CARLA projection (C/opt/projection.py:279-336)
-        + compute_controls' acc (C/opt/cem.py:307-309)."""
+        + compute_controls' acc (C/opt/cem.py:307-309).  det_obs = (x_obs,
+        y_obs): the det projection instead (C/opt/projection_det.py:279-336,
+        obstacle terms live; compute_cem_det, C/opt/cem.py:689-693)."""
         p = self.prob
         cxb, cyb = H.compute_x_guess(p, st["b_eq_x"], st["b_eq_y"], st["pop"])
-        from .projection import compute_projection
-        pr = compute_projection(p, st["b_eq_x"], st["b_eq_y"], st["lam_x"], st["lam_y"], cxb, cyb, st["s_lane"])
+        from .projection import compute_projection, compute_projection_det
+        if det_obs is None:
+            pr = compute_projection(p, st["b_eq_x"], st["b_eq_y"], st["lam_x"], st["lam_y"], cxb, cyb, st["s_lane"])
+        else:
+            pr = compute_projection_det(p, st["b_eq_x"], st["b_eq_y"], st["lam_x"], st["lam_y"], cxb, cyb,
+                                        st["s_lane"], det_obs[0], det_obs[1])
         st["lam_x"], st["lam_y"], st["s_lane"] = pr["lam_x"], pr["lam_y"], pr["s_lane"]
         arc = np.asarray(path["arc_vec"], F32)
         xs = np.clip(pr["x"], F32(0), arc[-1])
@@ -487,6 +495,8 @@ class CarlaCEM(CEM):
         p = self.prob
         if cost == "mmd_opt":
             return p.weight_mmd_obs, p.weight_mmd_lane, p.weight_mmd_lane_des
+        if cost == "det":                     # 0 * the zero risks (C/opt/cem.py:750)
+            return 0.0, 0.0, 0.0
         return p.weight_cvar_obs, p.weight_cvar_lane, p.weight_cvar_lane_des
 
     def select_carla(self, cost, st, t, pr, steer, obs, lane, des, v_des, draws, extra):
@@ -529,6 +539,36 @@ class CarlaCEM(CEM):
                 trace.append(dict(res_norm=pr["res_norm"], obs=obs, lane=lane, des=des, steer=steer,
                                   kappa=pr["kappa"], acc=acc, pop=st["pop"].copy(), mean=st["mean"].copy(),
                                   **info, **{k: v for k, v in extra.items() if k != "frenet"}))
+        xd = basis_eval(p.Pdot, out["cx"][None])[0]
+        yd = basis_eval(p.Pdot, out["cy"][None])[0]
+        v_best = np.sqrt(xd * xd + yd * yd).astype(F32)
+        return out["cx"], out["cy"], v_best, out["steer"].astype(F32), st["mean"].copy(), out
+
+    # -- compute_cem_det (C/opt/cem.py:633-790) --------------------------------
+    def select_det(self, st, t, pr, steer, v_des, draws):
+        """The det iteration after the projection (C/opt/cem.py:695-772): no
+        rollouts; the obstacle "cost" is zeros, so its stable argsort keeps the
+        projection order and the elites are its first 20 (:720-722); the cost
+        has zero risk terms (:750)."""
+        p = self.prob
+        B = pr["res_norm"].shape[0]
+        z = np.zeros(B, F32)
+        return self.select_carla("det", st, t, pr, steer, z, z, z, v_des, draws, {})
+
+    def solve_det(self, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des, path, draws, trace=None, iters=None):
+        """compute_cem_det: (cx, cy, v_best [100], steering [100], mean_param [8], out)."""
+        p = self.prob
+        x_obs = np.asarray(x_obs, F32)
+        y_obs = np.asarray(y_obs, F32)
+        st = self.init_carla("det", init_state, mean, cov, path, draws)
+        out = None
+        for t in range(p.maxiter_cem if iters is None else iters):
+            pr, acc, steer = self.front_carla(st, path, det_obs=(x_obs, y_obs))
+            out, info = self.select_det(st, t, pr, steer, F32(v_des), draws)
+            if trace is not None:
+                trace.append(dict(res_norm=pr["res_norm"], steer=steer, kappa=pr["kappa"], acc=acc,
+                                  pop=st["pop"].copy(), mean=st["mean"].copy(), c_x=pr["c_x"], c_y=pr["c_y"],
+                                  lam_x=st["lam_x"].copy(), lam_y=st["lam_y"].copy(), **info))
         xd = basis_eval(p.Pdot, out["cx"][None])[0]
         yd = basis_eval(p.Pdot, out["cy"][None])[0]
         v_best = np.sqrt(xd * xd + yd * yd).astype(F32)

@@ -220,6 +220,26 @@ class Problem:
             fit = fit + gi[:, k][:, None] * Pp[:, k][None, :]
         self.fit = fit                                               # [11, H]
 
+    def det_kinv(self):
+        """KKT inverses of the CARLA det projection (``C/opt/projection_det.py:
+        149-160``): the cost matrices gain ``rho_obs A_obs^T A_obs`` with
+        ``A_obs = tile(P, (num_obs, 1))`` (``C/opt/cem.py:66``), accumulated row
+        by row over the O x 100 rows (host_constants.cpp: det_projection_kinv).
+        Returns (kinv_x [14, 14], kinv_y [15, 15]); cached."""
+        if getattr(self, "_det_kinv", None) is None:
+            P = self.P.astype(F64)
+            nv = self.nvar
+            A_obs = np.tile(P, (self.num_obs, 1))
+            obs = _atb(A_obs, A_obs)
+            base = (np.eye(nv) + _atb(self.Pddot.astype(F64), self.Pddot.astype(F64))) \
+                + _atb(self.Pdot.astype(F64), self.Pdot.astype(F64))
+            ne_x, ne_y = self.A_eq_x.shape[0], self.A_eq_y.shape[0]
+            kx = np.block([[base + obs, self.A_eq_x.T], [self.A_eq_x, np.zeros((ne_x, ne_x))]])
+            ky = np.block([[(base + _atb(self.A_lane, self.A_lane)) + obs, self.A_eq_y.T],
+                           [self.A_eq_y, np.zeros((ne_y, ne_y))]])
+            self._det_kinv = (gauss_jordan_inverse(kx), gauss_jordan_inverse(ky))
+        return self._det_kinv
+
     def kkt_rhs_const(self, kinv, b):
         """Kinv[:11, 11:] @ b_eq, sequential over the equality rows."""
         out = np.zeros(self.nvar)

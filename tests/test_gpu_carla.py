@@ -234,11 +234,66 @@ def test_carla_dropin_interface(native):
     cem = importlib.import_module(carla_package() + ".cem")
     prob = cem.CEM(4, 1, 3, 0.1, 60, "gaussian", "Town05", 0.0, 0.0)
     init, xo, yo, path = _tick(40, 3, 60)
-    for fn in (prob.compute_cem_mmd, prob.compute_cem_cvar):
+    for fn in (prob.compute_cem_mmd, prob.compute_cem_cvar, prob.compute_cem_det):
         cx, cy, v, steer, mean = fn(1, init, MEAN, COV, xo, yo, 10.0, path["x_path"], path["y_path"],
                                     path["arc_vec"], path["Fx_dot"], path["Fy_dot"], path["kappa"])
         assert cx.shape == (11,) and cy.shape == (11,) and v.shape == (100,) and steer.shape == (100,)
         assert mean.shape == (8,) and np.all(np.isfinite(cx)) and np.all(np.isfinite(steer))
         assert np.all(np.abs(steer) < np.pi / 2)
-    with pytest.raises(NotImplementedError):
-        prob.compute_cem_det()
+    # cem.py:161-166: only "Town10HD" selects its constants (Town10HD_Opt gets Town05's)
+    opt = cem.CEM(4, 1, 3, 0.1, 60, "gaussian", "Town10HD_Opt", 0.0, 0.0)
+    assert (opt.y_lb, opt.y_ub, opt.y_des_2) == (-3.8, 0.3, -3.5)
+
+
+@pytest.mark.parametrize("n,B,tick,town", [(10, 100, 60, "Town05"), (10, 100, 170, "Town10HD")])
+def test_carla_det_lockstep(native, n, B, tick, town):
+    """compute_cem_det (carla/optimizer/cem.py:633-790) against the oracle's
+    restatement of it and of projection_det.py, 20 free-running iterations at
+    the configs[4] shape (H = 60, B = 100, 3 obstacles): the projection with
+    its obstacle terms live, then the elites of the projection order with
+    zero risk terms.  Every iteration's projection order, elites and cost
+    elites exact; res_norm, steering, curvature and the multipliers within
+    fp32 rounding; the returned tuple within 1e-4."""
+    H, O, T, level = 60, 3, 20, 0.1
+    init, xo, yo, path = _tick(tick, O, H)
+    ora = K.CarlaCEM(n, 1, O, level, H, "gaussian", town, 0.0, 0.0, num_batch=B, maxiter_cem=T)
+    variant = "carla_town10hd" if town == "Town10HD" else "carla_town05"
+    cfg = native.make_config(n, O, level, H, "gaussian", 0.0, 0.0, num_batch=B, maxiter_cem=T, variant=variant)
+    for xy in ("x", "y"):   # the det KKT inverse (A_obs^T A_obs in the cost) bit-identical to the oracle's
+        assert np.array_equal(native.host_constant(cfg, f"det_kinv_{xy}"),
+                              ora.prob.det_kinv()[0 if xy == "x" else 1].reshape(-1))
+    nat = native.Handle(cfg)
+    idx = 5
+    draws = K.CarlaDraws.random(ora.prob, np.random.default_rng(11), idx_mpc=idx, with_beta_cem=False)
+    trace = []
+    ref = ora.solve_det(idx, init, MEAN, COV, xo, yo, 10.0, path, draws, trace=trace)
+    nat.carla_begin("det", idx, init, MEAN, COV, xo, yo, 10.0, path, draws)
+    st0 = ora.init_carla("det", init, MEAN, COV, path, draws)
+    assert np.array_equal(nat.read("st0r").reshape(-1, 8)[:1, :5], st0["rows0"]), "noisy initial state differs"
+    for t in range(T):
+        nat.iterate(t, 1)
+        nat.sync()
+        tr = trace[t]
+        close(f"res_norm[{t}]", nat.read("res_norm")[:B], tr["res_norm"], rtol=1e-5, atol=1e-6)
+        close(f"steer[{t}]", nat.read("steer").reshape(-1, 100)[:B], tr["steer"], rtol=1e-4, atol=1e-5)
+        close(f"kappa[{t}]", nat.read("kappa_i").reshape(-1, 100)[:B], tr["kappa"], rtol=1e-4, atol=1e-6)
+        close(f"lam_x[{t}]", nat.read("lam_x").reshape(-1, 11)[:B], tr["lam_x"], rtol=1e-4, atol=1e-3)
+        close(f"lam_y[{t}]", nat.read("lam_y").reshape(-1, 11)[:B], tr["lam_y"], rtol=1e-4, atol=1e-3)
+        tp = nat.read("tr_proj", np.int32).reshape(T, B)[t]
+        to = nat.read("tr_obs", np.int32).reshape(T, 20)[t]
+        tc = nat.read("tr_cem", np.int32).reshape(T, 5)[t]
+        assert np.array_equal(tp, tr["perm"]), f"iteration {t}: projection order differs"
+        assert np.array_equal(to, tr["perm"][:20]) and np.array_equal(to, tr["elite_obs"]), \
+            f"iteration {t}: det elites are the projection order's first 20"
+        assert np.array_equal(tc, tr["elite_cem"]), f"iteration {t}: cost elites {tc} vs {tr['elite_cem']}"
+        close(f"mean[{t}]", nat.read("mean")[:8], tr["mean"], rtol=1e-4, atol=1e-5)
+    got = nat.finish()
+    cx, cy, v_best, steer_best, mean_param, out = ref
+    close("cx", got["cx"], cx, rtol=1e-4, atol=1e-4)
+    close("cy", got["cy"], cy, rtol=1e-4, atol=1e-4)
+    close("v_best", got["v_best"], v_best, rtol=1e-4, atol=1e-4)
+    close("steering", got["steering"], steer_best, rtol=1e-4, atol=1e-5)
+    close("mean_param", got["mean_param"], mean_param, rtol=1e-4, atol=1e-4)
+    assert float(got["cost_obs"]) == 0.0 and float(got["cost_lane"]) == 0.0
+    print(f"CARLA det n={n} B={B} {town} tick {tick}: 20 iterations in lockstep; res_norm range "
+          f"{float(trace[-1]['res_norm'].min()):.3f}..{float(trace[-1]['res_norm'].max()):.3f}")

@@ -77,3 +77,18 @@ def test_drop_in_package_imports_without_jax():
     assert hasattr(cem, "CEM")
     import sys
     assert "jax" not in sys.modules
+
+
+@pytest.mark.parametrize("O,variant", [(3, "carla_town05"), (7, "carla_town10hd")])
+def test_det_kkt_inverse_bit_identical(nat, O, variant):
+    """compute_cem_det's projection KKT (carla/optimizer/projection_det.py:
+    149-160: + rho_obs A_obs^T A_obs, A_obs = tile(P, (O, 1))), host-built,
+    bit-identical to the oracle's."""
+    cfg = nat.make_config(10, O, 0.1, 60, "gaussian", 0.0, 0.0, num_batch=100, variant=variant)
+    p = Problem(10, O, 0.1, 60, "gaussian", 0.0, 0.0, num_batch=100, variant=variant)
+    kx, ky = p.det_kinv()
+    assert np.array_equal(nat.host_constant(cfg, "det_kinv_x"), kx.reshape(-1))
+    assert np.array_equal(nat.host_constant(cfg, "det_kinv_y"), ky.reshape(-1))
+    # the obstacle rows change the system: not the plain projection's inverse
+    assert not np.array_equal(kx, p.proj_kinv_x)
+
