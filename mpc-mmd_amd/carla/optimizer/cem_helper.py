@@ -3,7 +3,9 @@ frame helpers ``carla/main_carla.py`` calls through ``prob.cem_helper``
 (``:275, 286, 345, 364-376, 387-392``).
 
 * ``path_spline`` / ``waypoint_generator`` (cem_helper.py:244-276) are NumPy /
-  SciPy in the reference too (cubic splines of the route by arc length).
+  SciPy in the reference too (cubic splines of the route by arc length);
+  pinned bit for bit to the reference's own functions executed on fixed
+  routes (tests/golden/make_carla_path_golden.py).
 * ``custom_path_smoothing``, ``compute_path_parameters``, the Frenet
   transforms run in libmpcmmd.so (host C++, the same operations as its
   kernels; include/mpcmmd.h).
@@ -61,7 +63,7 @@ class Helper:
         dx, dy = np.diff(x_path), np.diff(y_path)
         heading = np.unwrap(np.arctan2(dy, dx))
         heading = np.concatenate([heading[:1], heading])
-        arc_length = np.cumsum(np.hypot(dx, dy))[-1]
+        arc_length = np.cumsum(np.sqrt(dx ** 2 + dy ** 2))[-1]   # the reference's formula (not hypot: last-bit)
         arc_vec = np.linspace(0.0, arc_length, x_path.shape[0])
         return (CubicSpline(arc_vec, x_path), CubicSpline(arc_vec, y_path), CubicSpline(arc_vec, heading),
                 arc_length, arc_vec)
@@ -70,7 +72,7 @@ class Helper:
                            cs_y_path, cs_phi_path, arc_length):
         """num_path waypoints over the 300 m ahead of the route point closest
         to the ego (cem_helper.py:264-276)."""
-        d = np.hypot(x_global_init - np.asarray(x_path_data), y_global_init - np.asarray(y_path_data))
+        d = np.sqrt((x_global_init - np.asarray(x_path_data)) ** 2 + (y_global_init - np.asarray(y_path_data)) ** 2)
         s0 = arc_vec[int(np.argmin(d))]
         look = np.linspace(s0, s0 + 300.0, self.num_path)
         return cs_x_path(look), cs_y_path(look), cs_phi_path(look)

@@ -98,7 +98,7 @@ def compute_cem(prob, cx_m, cy_m, z0, z, trace=None):
     samples[:, M] = np.maximum(samples[:, M], F32(prob.sigma_clip))
     res = np.zeros(T, F32)
     out = None
-    Dm = distance_matrix(F) if M > 256 else None
+    Dm = distance_matrix(F)   # gathered per sample: the same bits as recomputing them (reduced_qp)
     for t in range(T):
         sigma = samples[:, M].copy()
         top = select_top(samples, M, n)
@@ -123,3 +123,77 @@ def compute_cem(prob, cx_m, cy_m, z0, z, trace=None):
         samples = samples_next
     beta_best, sigma_best, sel_best = out
     return beta_best, res, F32(sigma_best), sel_best
+
+
+def compute_cem_batch(prob, cx_m, cy_m, z0, z):
+    """``compute_cem`` for a batch of candidates at once (cx_m, cy_m [B, M,
+    11]): the same per-candidate operations, stacked (tests compare it with the
+    one-candidate form).  Returns beta [B, n], res [B, 20], sigma [B], sel
+    [B, n]."""
+    Bc, M = cx_m.shape[0], cx_m.shape[1]
+    n = prob.num_reduced
+    E = prob.num_ellite_beta
+    T = prob.maxiter_beta_cem
+    F = np.concatenate([cx_m, cy_m], axis=2).astype(F32)            # [B, M, 22]
+    Dm = l1_dist(F[:, :, None, :], F[:, None, :, :])                 # [B, M, M]
+    s0 = f32(np.sqrt(20.0) * z0.astype(F64))
+    s0[:, M] = np.maximum(s0[:, M], F32(prob.sigma_clip))
+    samples = np.broadcast_to(s0, (Bc,) + s0.shape).copy()          # [B, K, M+1]
+    K = samples.shape[1]
+    res = np.zeros((Bc, T), F32)
+    bi = np.arange(Bc)[:, None]
+    eye_n = F32(0.05) * np.eye(n, dtype=F32)
+    inv_m = F64(F32(1.0 / M))
+    out = None
+    for t in range(T):
+        sigma = samples[:, :, M].copy()                              # [B, K]
+        keys = sort_key(np.abs(samples[:, :, :M]))
+        top = np.argsort(keys, axis=2, kind="stable")[:, :, M - n:]  # [B, K, n]
+        D_mix = Dm[bi[:, :, None], top]                              # [B, K, n, M]
+        D_red = np.take_along_axis(D_mix, top[:, :, None, :], axis=3)
+        sig = sigma.astype(F32)[:, :, None, None]
+        K_red = np.exp((-D_red) / sig).astype(F32)
+        K_mix = np.exp((-D_mix) / sig).astype(F32)
+        g = K_mix.astype(F64).sum(axis=3) * inv_m                    # [B, K, n]
+        kkt = np.zeros((Bc, K, n + 1, n + 1))
+        kkt[:, :, :n, :n] = (K_red + eye_n).astype(F64)
+        kkt[:, :, :n, n] = 1.0
+        kkt[:, :, n, :n] = 1.0
+        rhs = np.concatenate([g, np.ones((Bc, K, 1))], axis=2)
+        beta = f32(np.linalg.solve(kkt.reshape(-1, n + 1, n + 1), rhs.reshape(-1, n + 1, 1))[:, :n, 0]
+                   ).reshape(Bc, K, n)
+        b = beta.astype(F64)
+        quad = np.einsum("ksi,ksij,ksj->ks", b, K_red.astype(F64), b)
+        cost = f32(quad + np.einsum("ksi,ksi->ks", -2.0 * g, b))
+        idx_e = np.argsort(sort_key(cost), axis=1, kind="stable")[:, :E]   # [B, E]
+        El = samples[bi, idx_e].astype(F64)                                # [B, E, M+1]
+        mean64 = El.mean(axis=1)
+        Dd = El - mean64[:, None, :]
+        cov = np.matmul(Dd.transpose(0, 2, 1), Dd) / (E - 1) + 0.05 * np.eye(M + 1)
+        L = np.linalg.cholesky(cov)
+        new = f32(f32(mean64).astype(F64)[:, None, :] + np.matmul(z[t].astype(F64)[None], L.transpose(0, 2, 1)))
+        samples_next = np.concatenate([samples[bi, idx_e], new], axis=1).astype(F32)
+        samples_next[:, :, M] = np.maximum(samples_next[:, :, M], F32(prob.sigma_clip))
+        nan = np.isnan(cost)
+        imin = np.where(nan.any(axis=1), np.argmax(nan, axis=1), np.argmin(np.where(nan, np.inf, cost), axis=1))
+        res[:, t] = np.where(nan.any(axis=1), np.nan, cost.min(axis=1))
+        out = (beta[np.arange(Bc), imin], samples_next[np.arange(Bc), imin, M], top[np.arange(Bc), imin])
+        samples = samples_next
+    beta_best, sigma_best, sel_best = out
+    return beta_best.copy(), res, sigma_best.astype(F32), sel_best.copy()
+
+
+def compute_cem_many(prob, cx_m, cy_m, z0, z, threads=8):
+    """``compute_cem_batch`` over candidate chunks on a thread pool (NumPy
+    releases the GIL in its array kernels; no processes, so nothing is forked
+    from a process that holds the GPU).  Same bits as one call."""
+    Bc = cx_m.shape[0]
+    k = max(1, min(threads, Bc))
+    if k == 1:
+        return compute_cem_batch(prob, cx_m, cy_m, z0, z)
+    from concurrent.futures import ThreadPoolExecutor
+    cuts = np.linspace(0, Bc, k + 1).astype(int)
+    with ThreadPoolExecutor(k) as ex:
+        parts = list(ex.map(lambda i: compute_cem_batch(prob, cx_m[cuts[i]:cuts[i + 1]], cy_m[cuts[i]:cuts[i + 1]],
+                                                        z0, z), range(k)))
+    return tuple(np.concatenate([p[j] for p in parts]) for j in range(4))

@@ -466,13 +466,9 @@ class CarlaCEM(CEM):
             acc_m, steer_m = H.mother_controls(acc_n, steer_n)
             xm, ym = rollout_cr(p, acc_m, steer_m, st["rows0"][None, :, :])
             cxm, cym = H.compute_coeff(p, xm, ym)
-            beta = np.empty((B, n), F32)
-            sigma = np.empty(B, F32)
-            res_beta = np.empty((B, p.maxiter_beta_cem), F32)
-            sel = np.empty((B, n), np.int64)
-            for b in range(B):
-                beta[b], res_beta[b], sigma[b], sel[b] = bc.compute_cem(p, cxm[b], cym[b], draws.beta_z0,
-                                                                       draws.beta_z)
+            # every candidate's beta-CEM, stacked and on a thread pool (the same
+            # bits as bc.compute_cem per candidate)
+            beta, res_beta, sigma, sel = bc.compute_cem_many(p, cxm, cym, draws.beta_z0, draws.beta_z, threads=4)
             xr = np.take_along_axis(xm, sel[:, :, None], axis=1)
             yr = np.take_along_axis(ym, sel[:, :, None], axis=1)
             sf, df = frenet_points(xr, yr, path)

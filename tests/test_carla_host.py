@@ -114,3 +114,27 @@ def test_town_constants_follow_the_reference():
         assert K.TOWNS.get(town, "carla_town05") == want
     ora = K.CarlaCEM(4, 1, 3, 0.1, 30, "gaussian", "Town10HD_Opt", 0.0, 0.0, num_batch=20, maxiter_cem=1)
     assert (ora.prob.y_lb, ora.prob.y_ub, ora.prob.y_des_2) == (-3.8, 0.3, -3.5)
+
+
+def test_route_helpers_pinned_to_reference():
+    """The drop-in's ``path_spline`` / ``waypoint_generator`` (carla/optimizer/
+    cem_helper.py:244-276 of the reference, NumPy / SciPy there too) against
+    the outputs of the reference's own functions EXECUTED on the same routes
+    (tests/golden/make_carla_path_golden.py): bit for bit."""
+    import importlib
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_gpu_carla import carla_package
+    Helper = importlib.import_module(carla_package() + ".cem_helper").Helper
+    g = np.load(os.path.join(ROOT, "tests", "golden", "carla_path_ref.npz"), allow_pickle=False)
+    h = Helper(num_prime=60)
+    for name in ("town05", "extended", "loop"):
+        x, y = g[f"{name}_x"], g[f"{name}_y"]
+        csx, csy, csphi, arc_length, arc_vec = h.path_spline(x, y)
+        assert arc_length == g[f"{name}_arc_length"] and np.array_equal(arc_vec, g[f"{name}_arc_vec"]), name
+        s = g[f"{name}_s"]
+        for k, cs in (("csx", csx), ("csy", csy), ("csphi", csphi)):
+            assert np.array_equal(cs(s), g[f"{name}_{k}"]), f"{name} {k}"
+        for e, ref in zip(g[f"{name}_ego"], g[f"{name}_wp"]):
+            wp = h.waypoint_generator(e[0], e[1], x, y, arc_vec, csx, csy, csphi, arc_length)
+            assert np.array_equal(np.stack(wp), ref), f"{name} waypoints at {e}"
