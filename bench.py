@@ -402,7 +402,7 @@ def run_carla(ticks, warmup, local, n=None):
     rec = rep.record_synthetic(ticks=(warmup + ticks) * stride + 1, town=w["town"])
     mean0 = np.array([10.0] * 4 + [0.0] * 4, np.float32)                  # main_carla.py:306-318
     cov = np.diag([20.0] * 4 + [100.0] * 4).astype(np.float32)
-    means = {"mmd_opt": mean0.copy(), "cvar": mean0.copy()}
+    means = {"mmd_opt": mean0.copy(), "cvar": mean0.copy(), "det": mean0.copy()}
     rows = []
     for i in range(warmup + ticks):
         k = i * stride
@@ -414,9 +414,14 @@ def run_carla(ticks, warmup, local, n=None):
         t2 = time.perf_counter()
         r2 = prob.compute_cem_cvar(k, init, means["cvar"], cov, xo, yo, 10.0, *args)
         t3 = time.perf_counter()
-        means["mmd_opt"], means["cvar"] = r1[4], r2[4]
+        # compute_cem_det (main_carla.py:194, --costs det): the deterministic
+        # baseline of the same tick, timed on its own (not part of the
+        # mmd + cvar tick)
+        r3 = prob.compute_cem_det(k, init, means["det"], cov, xo, yo, 10.0, *args)
+        t4 = time.perf_counter()
+        means["mmd_opt"], means["cvar"], means["det"] = r1[4], r2[4], r3[4]
         if i >= warmup:
-            rows.append((t1 - t0, t2 - t1, t3 - t2, t3 - t0))
+            rows.append((t1 - t0, t2 - t1, t3 - t2, t3 - t0, t4 - t3))
     torch.cuda.synchronize()
     a = np.array(rows) * 1e3
     # one profiled tick: per-kernel HIP-event times of both solves
@@ -456,6 +461,7 @@ def run_carla(ticks, warmup, local, n=None):
             "ticks_within_budget": float(np.mean(a[:, 3] <= w["budget_ms"])),
             "ms_preprocess": float(np.mean(a[:, 0])), "ms_mmd": float(np.mean(a[:, 1])),
             "ms_cvar": float(np.mean(a[:, 2])),
+            "ms_det": float(np.mean(a[:, 4])), "median_ms_det": float(np.median(a[:, 4])),
             "ms_per_tick_two_streams": float(np.mean(conc)),
             "profiled_tick_gpu_ms": gpu_ms,
             "kernels_ms_per_tick": {k: v[1] for k, v in kt.items()},
@@ -518,7 +524,12 @@ def main():
                        "global_batch": w["num_batch"] * world, "num_batch": w["num_batch"],
                        "num_prime": w["num_prime"], "num_obs": w["num_obs"], "num_reduced": w["num_reduced"],
                        "noise": w["noise"], "noise_level": w["level"], "parallelism": f"config-sharded x{world}",
-                       "solves_per_s": value / T},
+                       "solves_per_s": value / T,
+                       # dtype f32 is the reference's arithmetic (JAX default); parts of the path run wider
+                       "wider_arithmetic": ("beta-CEM sampler k_bsample: fp64 MFMA (v_mfma_f64_16x16x4); "
+                                            "KKT / basis products, projection transcendentals, Beta sampling: fp64"
+                                            if w["cost"] == "mmd_opt" else
+                                            "KKT / basis products, projection transcendentals, Beta sampling: fp64")},
             "median_ms_per_step": float(np.median(r["step_ms"])),
             "roofline": r["roof"],
             "kernels_ms_per_step": r["kernels"],
@@ -539,6 +550,8 @@ def main():
                                "median_ms_per_step": float(np.median(x["step_ms"])),
                                "solves_per_s": steps / x["elapsed"] / T, "roofline": x["roof"],
                                "kernels_ms_per_step": x["kernels"]}
+                if name == "cvar" and a.cpu_seconds > 0:   # configs[2]: the workload where 10k steps/s is reachable
+                    extra[name]["cpu_baseline"] = cpu_baseline(x["w"], x["inst"], min(a.cpu_seconds, 10.0))
             for nn in (10, 22):  # configs[4]: num_reduced_set 10 (the line's workload) and 22 (configs[1]'s n)
                 extra["carla" if nn == 10 else f"carla_n{nn}"] = run_carla(ticks=10, warmup=2, local=local, n=nn)
             line["extra_workloads"] = extra

@@ -1044,6 +1044,41 @@ __global__ __launch_bounds__(64 * kChunkWavesMax) void k_bsample_chunks(Params p
   MPCMMD_STAMP(p, 1);
 }
 
+// One tile of 16 samples of candidate b, every block walked by the calling
+// wave (k_bsample's walker with one tile per wave, its chunk folds included:
+// the same operations per tile, so the same bits).  k_bcem_small's sampler.
+DEVI void bsample_tile(const Params& p, int tb, int b, int tile) {
+  const int M = p.M, Pp = pos_pad(M), nblk = Pp >> 4, cl = sample_chunk(nblk);
+  const int lane = threadIdx.x & 63, r = lane & 15, h = lane >> 4, s0 = tile * 16;
+  const double* G = p.gen + size_t(b) * Pp * kGenStride;
+  const double* GU = G + gen_uplane(Pp);
+  const double* gm = p.genm + size_t(b) * Pp;
+  const float* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
+  const int ys = ygen_stride(M);
+  float* plane = p.ygen + size_t(b) * kBzCols * ys;
+  d4 S[1] = {d4{0.0, 0.0, 0.0, 0.0}}, Sp[1] = {d4{0.0, 0.0, 0.0, 0.0}}, Ya[1], Yb[1];
+  Sp[0][2] = h == 3 ? 1.0 : 0.0;  // row 11 of S_pre: the mean's coefficient
+  SampleBlock<1> qa, qb;
+  load_block(qa, G, GU, gm, z, 0, s0, r, h);
+  for (int c = 0; c < nblk; c += 2) {
+    const int p0 = c << 4;
+    load_block(qb, G, GU, gm, z, p0 + 16, s0, r, h);
+    __builtin_amdgcn_sched_barrier(0);
+    block_mfma(qa, S, Sp, Ya, r, h);
+    __builtin_amdgcn_sched_barrier(0);
+    if (c > 0) block_store<1>(Yb, plane, p0 - 16, M, ys, s0, r, h);
+    __builtin_amdgcn_sched_barrier(0);
+    load_block(qa, G, GU, gm, z, min(p0 + 32, Pp - 16), s0, r, h);
+    __builtin_amdgcn_sched_barrier(0);
+    block_mfma(qb, S, Sp, Yb, r, h);
+    if ((c + 2) % cl == 0) fold_chunk(Sp[0], S[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    block_store<1>(Ya, plane, p0, M, ys, s0, r, h);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  block_store<1>(Yb, plane, Pp - 16, M, ys, s0, r, h);
+}
+
 // ------------------------------------------------------------------------
 // k_bselect: top-n |beta| rows (compute_beta.py:117-118) and sigma of the
 // 100 samples.  Single-wave workgroups, W = gridDim.y waves per candidate;
@@ -1051,12 +1086,12 @@ __global__ __launch_bounds__(64 * kChunkWavesMax) void k_bsample_chunks(Params p
 // NQ = keys per lane (M <= 64 NQ), R = window capacity / 64, G = groups for
 // the window threshold (0: bisection): one instantiation per size, so each
 // has its own register allocation
+// the samples g, g + W, ... of candidate b on the calling wave; cand [64 R +
+// 8], lm [64], scratch [128]: the wave's LDS
 template <int NQ, int R, int G>
-__global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
-  __shared__ __attribute__((aligned(16))) unsigned long long cand[64 * R + 8];
-  __shared__ __attribute__((aligned(16))) uint32_t lm[64];
-  __shared__ int scratch[128];
-  const int b = p.b0 + blockIdx.x, g = blockIdx.y, W = gridDim.y, M = p.M, M1 = M + 1, n = p.n;
+DEVI void bselect_wave(const Params& p, int tb, int b, int g, int W, unsigned long long* cand, uint32_t* lm,
+                       int* scratch) {
+  const int M = p.M, M1 = M + 1, n = p.n;
   int32_t* sel = p.bsel + size_t(b) * kBetaSamples * n;
   float* sig = p.bsig + size_t(b) * kBetaSamples;
   const float* E = p.belite + (size_t(tb & 1) * p.Bt + b) * kBetaElite * M1;
@@ -1075,10 +1110,19 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
   const int s_lo = first_sample(tb);
   if (s_lo + g >= kBetaSamples) return;
   select_walk<NQ, R, G>(row, [&](int s) { return sel + s * n; }, s_lo + g, kBetaSamples, W, M, n, cand, lm, scratch);
-  for (int s = s_lo + g + int(threadIdx.x) * W; threadIdx.x < 16 && s < kBetaSamples; s += 16 * W) {
+  const int lane = threadIdx.x & 63;
+  for (int s = s_lo + g + lane * W; lane < 16 && s < kBetaSamples; s += 16 * W) {
     const float v = row(s)(M);
     sig[s] = tb == 0 ? fmaxf(v, 0.01f) : v;  // later rows are clipped when written
   }
+}
+
+template <int NQ, int R, int G>
+__global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
+  __shared__ __attribute__((aligned(16))) unsigned long long cand[64 * R + 8];
+  __shared__ __attribute__((aligned(16))) uint32_t lm[64];
+  __shared__ int scratch[128];
+  bselect_wave<NQ, R, G>(p, tb, p.b0 + blockIdx.x, blockIdx.y, gridDim.y, cand, lm, scratch);
 }
 
 // ------------------------------------------------------------------------
@@ -1155,7 +1199,7 @@ HDI KerLds ker_lds(int M, int n, size_t scratch) {
   L.total = take.o;
   return L;
 }
-HDI size_t ker_sample_bytes(int n) { return size_t(kKerWaves) * n * kFeatStride * 4; }
+HDI size_t ker_sample_bytes(int n, int nw = kKerWaves) { return size_t(nw) * n * kFeatStride * 4; }
 HDI size_t ker_tab_bytes(int U) { return ((size_t(U) * (U - 1) / 2 * 4 + 15) & ~size_t(15)) + size_t(U) * kFeatStride * 4; }
 constexpr size_t kKerTabBytes = 55 * 1024;  // the table of a union of <= 144 rows
 // scratch: the series records of every mother row (up to kKerRecBytes;
@@ -1163,8 +1207,8 @@ constexpr size_t kKerTabBytes = 55 * 1024;  // the table of a union of <= 144 ro
 // kKerTabBytes) from the second beta-iteration on (the first one's 100 fresh
 // samples select nearly every mother row)
 constexpr size_t kKerRecBytes = 64 * 1024;
-HDI size_t ker_scratch(int M, int n, int tb) {
-  size_t sc = ker_sample_bytes(n);
+HDI size_t ker_scratch(int M, int n, int tb, int nw = kKerWaves) {
+  size_t sc = ker_sample_bytes(n, nw);
   size_t rec = size_t(M) * kMomStride * 4;
   if (rec > kKerRecBytes) rec = kKerRecBytes;
   if (rec > sc) sc = rec;
@@ -1241,12 +1285,12 @@ DEVI float series_sum(const float4 (&q)[3], double na) {
 }
 static_assert(kMomR == 12 && kMom == 12, "record layout: P_0..P_11 in float4s 0..2, R in float4 3");
 
-// two workgroups per CU: 8 waves per SIMD, which needs <= 64 VGPRs and <= 80
-// SGPRs (MI355X_MICROARCH.md residency rules: 90 SGPRs admitted one)
-__global__ __launch_bounds__(64 * kKerWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_bkernel(Params p, int tb, int split, int scratch) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+// The body of k_bkernel for part `part` of candidate `cand` (of `split`),
+// NW waves (k_bkernel: 16; the small-batch fused kernel k_bcem_small: 8)
+template <int NW>
+DEVI void bkernel_body(const Params& p, int tb, int cand, int part, int split, int scratch, char* smem) {
+  constexpr int kKerWaves = NW;
   constexpr int NT = 64 * kKerWaves, Q = kFeatStride / 4;
-  const int cand = blockIdx.x / split, part = blockIdx.x - cand * split;
   const int b = p.b0 + cand, M = p.M, n = p.n;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1465,16 +1509,29 @@ __global__ __launch_bounds__(64 * kKerWaves) __attribute__((amdgpu_waves_per_eu(
   MPCMMD_STAMPW(p, 4);
 }
 
-template <int NV4>
-__global__ __launch_bounds__(64 * kDirWaves) void k_bdirect(Params p, int tb, int kparts, int split, int lpt) {
-  constexpr bool kPrefetch = NV4 <= 4;
-  constexpr int NT = 64 * kDirWaves;
+// two workgroups per CU: 8 waves per SIMD, which needs <= 64 VGPRs and <= 80
+// SGPRs (MI355X_MICROARCH.md residency rules: 90 SGPRs admitted one)
+__global__ __launch_bounds__(64 * kKerWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_bkernel(Params p, int tb, int split, int scratch) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int cand = blockIdx.x / split, part = blockIdx.x - cand * split;
-  const int b = p.b0 + cand, M = p.M, n = p.n, Md = dist_stride(M);
-  int total = 0;  // flagged pairs of the candidate (k_bkernel's parts)
+  bkernel_body<kKerWaves>(p, tb, cand, part, split, scratch, smem);
+}
+
+// flagged pairs of candidate b (k_bkernel's parts): k_bdirect's work
+DEVI int bdirect_total(const Params& p, int b, int kparts) {
+  int total = 0;
   for (int k = 0; k < kparts; ++k) total += p.bdcount[size_t(b) * kMaxSplit + k];
-  if (total == 0) return;  // block-uniform
+  return total;
+}
+
+// The body of k_bdirect for part `part` of candidate `cand` with `total` > 0
+// flagged pairs, NW waves (k_bdirect: 4; k_bcem_small: 8)
+template <int NV4, int NW>
+DEVI void bdirect_body(const Params& p, int tb, int split, int lpt, int cand, int part, int total, char* smem) {
+  constexpr int kDirWaves = NW;
+  constexpr bool kPrefetch = NV4 <= 4;
+  constexpr int NT = 64 * kDirWaves;
+  const int b = p.b0 + cand, M = p.M, n = p.n, Md = dist_stride(M);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const DirLds C = dir_lds(M, n);
@@ -1656,6 +1713,15 @@ __global__ __launch_bounds__(64 * kDirWaves) void k_bdirect(Params p, int tb, in
   MPCMMD_STAMP(p, 20);
 }
 
+template <int NV4>
+__global__ __launch_bounds__(64 * kDirWaves) void k_bdirect(Params p, int tb, int kparts, int split, int lpt) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int cand = blockIdx.x / split, part = blockIdx.x - cand * split;
+  const int total = bdirect_total(p, p.b0 + cand, kparts);
+  if (total == 0) return;  // block-uniform
+  bdirect_body<NV4, kDirWaves>(p, tb, split, lpt, cand, part, total, smem);
+}
+
 // ------------------------------------------------------------------------
 // k_bqp: compute_beta_reduced (compute_beta.py:70-91) for every sample:
 // C = K_red + 0.05 I, C x1 = g, C x2 = 1, beta = x1 + ((1 - sum x1) / sum x2) x2
@@ -1709,15 +1775,9 @@ DEVI float rsqrt_nr(float x) {
 // threads copy consecutive entries of one QP's triangle: coalesced), so the
 // per-lane row gathers of the factorisation and the cost read LDS, not
 // scattered global lines.
-template <int NP>
-DEVI void bqp_quad(const Params& p, int tb, float* kl) {
-  constexpr int T4 = NP / 4;
-  const int n = p.n, M = p.M, q = threadIdx.x & 3;
+DEVI void bqp_stage(const Params& p, int tb, float* kl) {
+  const int n = p.n;
   const int s_lo = first_sample(tb), per = kBetaSamples - s_lo;
-  const int gq = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;
-  const bool ok = gq < p.nb * per;
-  const int gqc = ok ? gq : 0;
-  const int b = p.b0 + gqc / per, s = s_lo + gqc % per;
   const int ntri = tri_stride(n);
   {  // the workgroup's K_red rows as float4s, consecutive threads on consecutive
      // float4s, every thread's loads issued before its first LDS store (one
@@ -1743,7 +1803,15 @@ DEVI void bqp_quad(const Params& p, int tb, float* kl) {
     }
     __syncthreads();
   }
-  const float* kr = kl + (threadIdx.x >> 2) * ntri;
+}
+
+// QP of sample s of candidate b on the calling quad (lane q = threadIdx.x & 3),
+// its K_red strict lower triangle at kr (LDS staging or global); ok = false:
+// compute on the clamped inputs, store nothing
+template <int NP>
+DEVI void bqp_solve(const Params& p, int b, int s, bool ok, const float* kr) {
+  constexpr int T4 = NP / 4;
+  const int n = p.n, M = p.M, q = threadIdx.x & 3;
   const float* br = p.brow + (size_t(b) * kBetaSamples + s) * n;
   const double inv_m = double(1.0f / float(M));
   const float cdiag = 1.0f + 0.05f;
@@ -1889,6 +1957,17 @@ DEVI void bqp_quad(const Params& p, int tb, float* kl) {
   if (q == 0) p.bcost[size_t(b) * kBetaSamples + s] = float(c1 - 2.0 * c3);
 }
 
+template <int NP>
+DEVI void bqp_quad(const Params& p, int tb, float* kl) {
+  const int s_lo = first_sample(tb), per = kBetaSamples - s_lo;
+  const int gq = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  const bool ok = gq < p.nb * per;
+  const int gqc = ok ? gq : 0;
+  const int b = p.b0 + gqc / per, s = s_lo + gqc % per;
+  bqp_stage(p, tb, kl);
+  bqp_solve<NP>(p, b, s, ok, kl + (threadIdx.x >> 2) * tri_stride(p.n));
+}
+
 HDI int qp_np(int n) { return n <= 8 ? 8 : (n <= 16 ? 16 : (n <= 24 ? 24 : (n <= 32 ? 32 : (n <= 48 ? 48 : 64)))); }
 // threads per workgroup: 32 QPs (their K_red in LDS: 30 KB at n = 22), 16 QPs
 // for n > 24 (32 KB at n = 32, so the LDS still admits 4 workgroups per CU)
@@ -2010,9 +2089,9 @@ HDI EliteLds elite_lds(int M1) {
 // packed upper index of (a <= c) in an 11 x 11 symmetric matrix
 HDI int sym11(int a, int c) { return a * 11 - a * (a - 1) / 2 + (c - a); }
 
-__global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int b = p.b0 + blockIdx.x, M = p.M, M1 = M + 1, n = p.n, tid = threadIdx.x;
+// The body of k_belite for candidate b (kThreads threads)
+DEVI void belite_body(const Params& p, int tb, int b, char* smem) {
+  const int M = p.M, M1 = M + 1, n = p.n, tid = threadIdx.x;
   const EliteLds C = elite_lds(M1);
   double* Gb = reinterpret_cast<double*>(smem + C.Gb);
   int* elite = reinterpret_cast<int*>(smem + C.misc);    // [11]
@@ -2204,6 +2283,11 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
   }
 }
 
+__global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  belite_body(p, tb, p.b0 + blockIdx.x, smem);
+}
+
 // k_bgen: level 2 of the generators, one quad (4 lanes) per (candidate,
 // block of 16 positions).  The block prefix Phi_b (k_belite) is inverted
 // once, A = Phi_b^-1; then, position by position through the block,
@@ -2220,12 +2304,11 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
 // give ~2 waves per SIMD at B = 1024 (one lane per block gave < 1).
 HDI int sym11i(int a, int c) { return a <= c ? sym11(a, c) : sym11(c, a); }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_bgen(Params p) {
+// the generators of 16-position block blk of candidate b on the calling quad
+// (lane q = threadIdx.x & 3); live = false: compute, store nothing
+DEVI void bgen_quad(const Params& p, int b, int blk, bool live) {
   const int M = p.M, M1 = M + 1, nblk = (M1 + 15) / 16;
-  const int gq = (blockIdx.x * blockDim.x + threadIdx.x) >> 2, q = threadIdx.x & 3;
-  const bool live = gq < p.nb * nblk;  // quads stay whole: dead ones compute on a clamped block, store nothing
-  const int gqc = live ? gq : p.nb * nblk - 1;
-  const int b = p.b0 + gqc / nblk, blk = gqc % nblk;
+  const int q = threadIdx.x & 3;
   double* gen = p.gen + size_t(b) * pos_pad(M) * kGenStride;
   const double* Gb = p.phib + (size_t(b) * nblk + blk) * 66;
   // own rows a = q + 4 i; row 11 (q = 3, i = 2) is padding: an identity row
@@ -2300,14 +2383,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   }
 }
 
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_bgen(Params p) {
+  const int nblk = (p.M + 1 + 15) / 16;
+  const int gq = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  const bool live = gq < p.nb * nblk;  // quads stay whole: dead ones compute on a clamped block, store nothing
+  const int gqc = live ? gq : p.nb * nblk - 1;
+  bgen_quad(p, p.b0 + gqc / nblk, gqc % nblk, live);
+}
+
 // k_bsigma (last beta-iteration only): sigma_best when argmin is a new
 // sample -- its sigma coordinate drawn with the NEW generators (Q4,
 // compute_beta.py:133-145): y_M = mean_M + L_MM z_M + u_M . sum_{j<M} w_j z_j
-__global__ __launch_bounds__(kThreads) void k_bsigma(Params p, int tb) {
-  __shared__ double red[(kThreads / 64) * 11];
-  const int b = p.b0 + blockIdx.x, M = p.M, tid = threadIdx.x;
+// the body of k_bsigma for candidate b when its argmin is a new sample;
+// red: (blockDim / 64) * 11 doubles of LDS
+DEVI void bsigma_body(const Params& p, int tb, int b, double* red) {
+  const int M = p.M, tid = threadIdx.x;
   const int imin = p.bimin[b];
-  if (imin < kBetaElite) return;  // k_belite wrote it
   const double* gen = p.gen + size_t(b) * pos_pad(M) * kGenStride;
   {
     const float* z = p.beta_z + size_t(tb) * pos_pad(M) * kBzCols;
@@ -2343,6 +2434,13 @@ __global__ __launch_bounds__(kThreads) void k_bsigma(Params p, int tb) {
       p.sigma[b] = fmaxf(yM, 0.01f);
     }
   }
+}
+
+__global__ __launch_bounds__(kThreads) void k_bsigma(Params p, int tb) {
+  __shared__ double red[(kThreads / 64) * 11];
+  const int b = p.b0 + blockIdx.x;
+  if (p.bimin[b] < kBetaElite) return;  // k_belite wrote it
+  bsigma_body(p, tb, b, red);
 }
 
 // ------------------------------------------------------------------------
@@ -2391,6 +2489,118 @@ __global__ __launch_bounds__(64) void k_mmdfinal(Params p, int t) {
 }
 
 
+// ------------------------------------------------------------------------
+// k_bcem_small: the 20 beta-iterations of one candidate in one workgroup
+// (small batches: the reference's num_batch = 100, BASELINE configs[4]'s
+// CARLA solves).  At B = 100 the seven per-iteration kernels above run as
+// one latency-bound launch each (10-27 us for a few microseconds of work per
+// candidate, 140 launches per outer iteration); here the same phases follow
+// each other inside one launch, separated by workgroup barriers, with the
+// candidate's intermediates (samples, selections, K_red, generators) in
+// global memory that this workgroup alone touches -- L2-resident at this
+// size.  Every phase is the body of its multi-kernel counterpart (same
+// operations, so the same bits): samples by bsample_tile (a wave per tile),
+// selection by bselect_wave, kernel sums / K_red by bkernel_body, direct row
+// sums by bdirect_body, the QPs by bqp_solve (a quad each), elites by
+// belite_body, generators by bgen_quad, sigma_best by bsigma_body.
+// 8 waves (512 threads): the QP and generator phases need up to 256 VGPRs.
+constexpr int kSmallWaves = 8;
+constexpr int kSmallThreads = 64 * kSmallWaves;
+static_assert(kSmallThreads == kThreads, "belite_body / bsigma_body assume kThreads threads");
+HDI size_t small_sel_bytes(int R) { return size_t(64 * R + 8) * 8 + 64 * 4 + 128 * 4; }  // one wave's select LDS
+HDI size_t small_lds(int M, int n, int R) {
+  size_t b = size_t(kSmallWaves) * small_sel_bytes(R);
+  const size_t k = ker_lds(M, n, ker_scratch(M, n, 1, kSmallWaves)).total;
+  const size_t d = dir_lds(M, n).total, e = elite_lds(M + 1).total;
+  const size_t q = size_t(kBetaSamples) * tri_stride(n) * 4;  // the QPs' K_red
+  b = b > q ? b : q;
+  b = b > k ? b : k;
+  b = b > d ? b : d;
+  b = b > e ? b : e;
+  return b;
+}
+
+// an SGPR value the compiler cannot see through: each beta-iteration works on
+// its own copy of the shapes, so no phase's index arithmetic (the QP's 84
+// triangle addresses, say) is hoisted out of the iteration loop and kept live
+// across every other phase (spills)
+DEVI int opaque_s(int v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+
+template <int NQ, int R, int G, int NP, int NV4>
+__global__ __launch_bounds__(kSmallThreads) void k_bcem_small(Params p0) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int cand = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int tb = 0; tb < kBetaIters; ++tb) {
+    Params p = p0;
+    p.n = opaque_s(p0.n);
+    p.M = opaque_s(p0.M);
+    p.b0 = opaque_s(p0.b0);
+    const int b = p.b0 + cand, M = p.M, n = p.n;
+    const int ntri = tri_stride(n);
+    // samples of this iteration (compute_beta.py:51-68); the first ones are
+    // the shared initial draws (Q3), taken from the handle's selection table
+    if (tb > 0) {
+      if (w < kSampleTiles) bsample_tile(p, tb, b, w);
+      __syncthreads();
+      char* sw = smem + size_t(w) * small_sel_bytes(R);
+      unsigned long long* cand_l = reinterpret_cast<unsigned long long*>(sw);
+      uint32_t* lm = reinterpret_cast<uint32_t*>(sw + size_t(64 * R + 8) * 8);
+      int* scr = reinterpret_cast<int*>(sw + size_t(64 * R + 8) * 8 + 64 * 4);
+      bselect_wave<NQ, R, G>(p, tb, b, w, kSmallWaves, cand_l, lm, scr);
+    } else {
+      for (int e = tid; e < kBetaSamples * n; e += kSmallThreads) p.bsel[size_t(b) * kBetaSamples * n + e] = p.sel0[e];
+      for (int e = tid; e < kBetaSamples; e += kSmallThreads) p.bsig[size_t(b) * kBetaSamples + e] = p.sig0[e];
+    }
+    __syncthreads();
+    // K_mixed row sums and K_red (compute_beta.py:120-127)
+    bkernel_body<kSmallWaves>(p, tb, cand, 0, 1, int(ker_scratch(M, n, tb, kSmallWaves)), smem);
+    __syncthreads();
+    if (tb > 0) {
+      const int total = bdirect_total(p, b, 1);  // block-uniform
+      if (total > 0) {
+        bdirect_body<NV4, kSmallWaves>(p, tb, 1, 1, cand, 0, total, smem);
+        __syncthreads();
+      }
+    }
+    // the QPs (compute_beta.py:70-91), a quad each, the samples' K_red staged
+    // in LDS (one contiguous copy: the candidate's triangles are consecutive)
+    {
+      const int s_lo = first_sample(tb), per = kBetaSamples - s_lo;
+      const float4* src = reinterpret_cast<const float4*>(p.bkred + (size_t(b) * kBetaSamples + s_lo) * ntri);
+      float4* kl4 = reinterpret_cast<float4*>(smem);
+      for (int i = tid; i < per * (ntri >> 2); i += kSmallThreads) kl4[i] = src[i];
+      __syncthreads();
+      static_assert(kSmallThreads / 4 >= kBetaSamples, "one quad per QP");
+      const int g = tid >> 2;
+      const bool ok = g < per;
+      const int gc = ok ? g : 0;
+      bqp_solve<NP>(p, b, s_lo + gc, ok, reinterpret_cast<const float*>(smem) + size_t(gc) * ntri);
+    }
+    __syncthreads();
+    // elites, mean, generator level 1 (compute_beta.py:51-68, 133-157)
+    belite_body(p, tb, b, smem);
+    __syncthreads();
+    // generator level 2, a quad per 16-position block
+    {
+      const int nblk = (M + 1 + 15) / 16;
+      for (int g0 = 0; g0 < nblk; g0 += kSmallThreads / 4) {
+        const int blk = g0 + (tid >> 2);
+        const bool live = blk < nblk;
+        bgen_quad(p, b, live ? blk : nblk - 1, live);
+      }
+    }
+    __syncthreads();
+    if (tb == kBetaIters - 1 && p.bimin[b] >= kBetaElite) {  // block-uniform
+      bsigma_body(p, tb, b, reinterpret_cast<double*>(smem));
+      __syncthreads();
+    }
+  }
+}
 
 }  // namespace
 
@@ -2575,6 +2785,23 @@ void launch_bgen(const Params& p, int tb, hipStream_t s) {
   const int nblk = (p.M + 1 + 15) / 16;
   hipLaunchKernelGGL(k_bgen, dim3((p.nb * nblk * 4 + 255) / 256), dim3(256), 0, s, p);
   if (tb == kBetaIters - 1) hipLaunchKernelGGL(k_bsigma, dim3(p.nb), dim3(kThreads), 0, s, p, tb);
+}
+
+bool bcem_small_ok(const Params& p) { return p.n <= 24 && p.nb <= 512; }
+
+void launch_bcem_small(const Params& p, hipStream_t s) {
+  const int n = p.n, M = p.M;
+  const dim3 grid(p.nb), block(kSmallThreads);
+  if (M <= 64)
+    hipLaunchKernelGGL((k_bcem_small<1, 1, 32, 8, 1>), grid, block, small_lds(M, n, 1), s, p);
+  else if (M <= 128)
+    hipLaunchKernelGGL((k_bcem_small<2, 1, 32, 16, 1>), grid, block, small_lds(M, n, 1), s, p);
+  else if (M <= 256)
+    hipLaunchKernelGGL((k_bcem_small<4, 1, 32, 16, 1>), grid, block, small_lds(M, n, 1), s, p);
+  else if (M <= 512)
+    hipLaunchKernelGGL((k_bcem_small<8, 1, 32, 24, 2>), grid, block, small_lds(M, n, 1), s, p);
+  else
+    hipLaunchKernelGGL((k_bcem_small<12, 1, 32, 24, 3>), grid, block, small_lds(M, n, 1), s, p);
 }
 
 void launch_mmdfinal(const Params& p, int t, hipStream_t s) {

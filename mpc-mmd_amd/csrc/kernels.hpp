@@ -273,6 +273,11 @@ void launch_bqp(const Params& p, int tb, hipStream_t s);
 void launch_belite(const Params& p, int tb, hipStream_t s);
 void launch_bgen(const Params& p, int tb, hipStream_t s);  // + k_bsigma on the last beta-iteration
 void launch_mmdfinal(const Params& p, int t, hipStream_t s);
+// the 20 beta-iterations of every candidate of [b0, b0 + nb) in one launch, a
+// workgroup per candidate (small batches, n <= 24; bit-identical to the
+// per-iteration kernels above)
+bool bcem_small_ok(const Params& p);
+void launch_bcem_small(const Params& p, hipStream_t s);
 bool mmdopt_supported(int n, int H, int O, std::string* why);
 // CARLA variant (k_carla.hip): rollouts of rows from their noisy initial
 // states (mode 0: the baseline rows of cvar; mode 1: the reduced set of

@@ -65,12 +65,13 @@ enum KernelId {
   kKRollCarla,
   kKFrenet,
   kKRiskCarla,
+  kKBcemSmall,
   kNumKernels
 };
 const char* kKernelNames[kNumKernels] = {"noise",   "front", "risk_baseline", "mother",   "bdist", "bsample",
                                          "bselect", "bkernel", "bqp",         "belite", "mmdfinal", "select",
                                          "gamma_tab", "beta_planes", "bgen",    "bmoment",     "bdirect",
-                                         "roll_carla", "frenet", "risk_carla"};
+                                         "roll_carla", "frenet", "risk_carla", "bcem_small"};
 
 }  // namespace
 
@@ -129,6 +130,9 @@ struct mpcmmd_handle {
   // gamma table drawn for another iteration (the table has one slot)
   bool ahead_on = true;
   int ahead_t = -1;
+  // small batches: the 20 beta-iterations as one launch (k_bcem_small);
+  // MPCMMD_FUSED=0 keeps the per-iteration kernels
+  bool fused_small = true;
   // profiling
   bool prof = false;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -335,6 +339,10 @@ void run_beta_iteration(mpcmmd_handle* h, const Params& p, int tb, hipStream_t s
 // so the HIP-event timings are per kernel)
 void run_beta_cem(mpcmmd_handle* h) {
   const int B = h->p.Bt;  // every candidate of every configuration
+  if (h->fused_small && bcem_small_ok(h->p)) {
+    h->launch(kKBcemSmall, [&] { launch_bcem_small(h->p, h->stream); });
+    return;
+  }
   // the default split applies to launches of >= 1024 candidates (a batch
   // handle may run fewer configurations than it holds); MPCMMD_GROUPS forces it
   const int G = h->prof ? 1 : (B >= 1024 || h->groups_forced ? h->groups : 1);
@@ -708,6 +716,7 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     h->groups_forced = std::getenv("MPCMMD_GROUPS") != nullptr;
     if (const char* g = std::getenv("MPCMMD_GRAPH")) h->graphs = std::atoi(g) != 0;
     if (const char* g = std::getenv("MPCMMD_AHEAD")) h->ahead_on = std::atoi(g) != 0;
+    if (const char* g = std::getenv("MPCMMD_FUSED")) h->fused_small = std::atoi(g) != 0;
     if (const char* g = std::getenv("MPCMMD_BETA_DUMP")) p.beta_dump = std::atoi(g) != 0;
     p.risk_rows = 1;  // the row-lane path is the faster one at configs[2]; MPCMMD_RISK_FUSED=1: fused
     if (const char* g = std::getenv("MPCMMD_RISK_FUSED")) p.risk_rows = std::atoi(g) == 0;
