@@ -94,6 +94,7 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
   const Cfg cf = cfg_of(p, b / p.B);
   float* an = reinterpret_cast<float*>(smem);
   float* sn = an + n * H;
+  float* tn = sn + n * H;  // CARLA: float(tan(double(steer))) of each control, off the rows' step chains
   float* gctrl = p.ctrl_n + size_t(b) * 2 * n * H;
   for (int idx = threadIdx.x; idx < n * H; idx += blockDim.x) {
     const int r = idx / H, h = idx % H;
@@ -101,6 +102,7 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
     noisy_control(p, cf, t, r, h, p.acc[size_t(b) * 100 + h], p.steer[size_t(b) * 100 + h], a, s);
     an[idx] = a;
     sn[idx] = s;
+    if (p.carla) tn[idx] = float(tan(double(s)));
     gctrl[idx] = a;
     gctrl[n * H + idx] = s;
   }
@@ -110,6 +112,7 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
     // jnp.repeat(acc, n, 0) / jnp.tile(steer, (n, 1)) (cem_helper.py:510-511)
     const float* ar = an + (m / n) * H;
     const float* sr = sn + (m % n) * H;
+    const float* tr = tn + (m % n) * H;
     // CARLA: every mother row starts from its own noisy initial state
     // (carla/optimizer/cem.py:251-253, cem_helper.py:846)
     const float* st = p.carla ? p.st0r + (size_t(cf.g) * p.R0 + m) * 8 : cf.st0;
@@ -126,7 +129,7 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
         cy[k] = cy[k] + f * dy;
       }
       if (h == H - 1) break;
-      if (p.carla) bicycle_step_cr(x, y, vx, vy, psi, ar[h], sr[h], p.wheel_base);
+      if (p.carla) bicycle_step_cr_t(x, y, vx, vy, psi, ar[h], tr[h], p.wheel_base);
       else bicycle_step(x, y, vx, vy, psi, ar[h], sr[h]);
     }
     float fr[kFeatStride];
@@ -1045,38 +1048,62 @@ __global__ __launch_bounds__(64 * kChunkWavesMax) void k_bsample_chunks(Params p
 }
 
 // One tile of 16 samples of candidate b, every block walked by the calling
-// wave (k_bsample's walker with one tile per wave, its chunk folds included:
-// the same operations per tile, so the same bits).  k_bcem_small's sampler.
-DEVI void bsample_tile(const Params& p, int tb, int b, int tile) {
+// wave: k_bsample's walker with one tile per wave, its chunk folds included
+// (the same operands and operations per block, so the same bits), the
+// candidate's generators read from an LDS copy (lg: W plane, U plane, genm,
+// as in global memory) and the normals kZAhead blocks ahead in registers, so
+// the per-block wait is the MFMA chain, not a global load.  k_bcem_small's
+// sampler (its workgroup just wrote the generators).
+constexpr int kZAhead = 4;
+HDI size_t gen_lds_bytes(int M) { return size_t(pos_pad(M)) * (2 * kGenRow + 1) * 8 + 16 * 8; }  // + wA's overreach
+DEVI void bsample_tile_lds(const Params& p, int tb, int b, int tile, const double* lg) {
   const int M = p.M, Pp = pos_pad(M), nblk = Pp >> 4, cl = sample_chunk(nblk);
   const int lane = threadIdx.x & 63, r = lane & 15, h = lane >> 4, s0 = tile * 16;
-  const double* G = p.gen + size_t(b) * Pp * kGenStride;
-  const double* GU = G + gen_uplane(Pp);
-  const double* gm = p.genm + size_t(b) * Pp;
+  const double* LW = lg;
+  const double* LU = lg + gen_uplane(Pp);
+  const double* LL = lg + 2 * gen_uplane(Pp);
   const float* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
   const int ys = ygen_stride(M);
   float* plane = p.ygen + size_t(b) * kBzCols * ys;
-  d4 S[1] = {d4{0.0, 0.0, 0.0, 0.0}}, Sp[1] = {d4{0.0, 0.0, 0.0, 0.0}}, Ya[1], Yb[1];
+  d4 S[1] = {d4{0.0, 0.0, 0.0, 0.0}}, Sp[1] = {d4{0.0, 0.0, 0.0, 0.0}}, Y[1];
   Sp[0][2] = h == 3 ? 1.0 : 0.0;  // row 11 of S_pre: the mean's coefficient
-  SampleBlock<1> qa, qb;
-  load_block(qa, G, GU, gm, z, 0, s0, r, h);
-  for (int c = 0; c < nblk; c += 2) {
-    const int p0 = c << 4;
-    load_block(qb, G, GU, gm, z, p0 + 16, s0, r, h);
-    __builtin_amdgcn_sched_barrier(0);
-    block_mfma(qa, S, Sp, Ya, r, h);
-    __builtin_amdgcn_sched_barrier(0);
-    if (c > 0) block_store<1>(Yb, plane, p0 - 16, M, ys, s0, r, h);
-    __builtin_amdgcn_sched_barrier(0);
-    load_block(qa, G, GU, gm, z, min(p0 + 32, Pp - 16), s0, r, h);
-    __builtin_amdgcn_sched_barrier(0);
-    block_mfma(qb, S, Sp, Yb, r, h);
-    if ((c + 2) % cl == 0) fold_chunk(Sp[0], S[0]);
-    __builtin_amdgcn_sched_barrier(0);
-    block_store<1>(Ya, plane, p0, M, ys, s0, r, h);
-    __builtin_amdgcn_sched_barrier(0);
+  auto zload = [&](float (&zz)[4], int c) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) zz[k] = z[bz_index(c * 16 + 4 * k + h, s0 + r)];
+  };
+  auto gload = [&](SampleBlock<1>& q, int p0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q.wA[k] = LW[size_t(p0 + 4 * k + h) * kGenRow + kGenW + r];
+    const double* g = LW + size_t(p0 + r) * kGenRow;
+    const double* gu = LU + size_t(p0 + r) * kGenRow;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      q.wX[i] = g[kGenW + 4 * i + h];
+      q.uX[i] = gu[4 * i + h];
+    }
+    q.L = LL[p0 + r];
+  };
+  float zr[kZAhead][4];
+#pragma unroll
+  for (int u = 0; u < kZAhead; ++u) zload(zr[u], min(u, nblk - 1));
+  SampleBlock<1> q[2];
+  gload(q[0], 0);
+  for (int c = 0; c < nblk; c += kZAhead) {
+#pragma unroll
+    for (int u = 0; u < kZAhead; ++u) {
+      const int cb = c + u;
+      if (cb < nblk) {  // wave-uniform
+        SampleBlock<1>& cur = q[u & 1];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cur.z[0][k] = zr[u][k];
+        zload(zr[u], min(cb + kZAhead, nblk - 1));
+        gload(q[(u + 1) & 1], min(cb + 1, nblk - 1) * 16);
+        block_mfma(cur, S, Sp, Y, r, h);
+        if ((cb + 1) % cl == 0) fold_chunk(Sp[0], S[0]);  // the walker's fold after the chunk's last block
+        block_store<1>(Y, plane, cb * 16, M, ys, s0, r, h);
+      }
+    }
   }
-  block_store<1>(Yb, plane, Pp - 16, M, ys, s0, r, h);
 }
 
 // ------------------------------------------------------------------------
@@ -2391,6 +2418,175 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   bgen_quad(p, p.b0 + gqc / nblk, gqc % nblk, live);
 }
 
+// The generators of block blk of candidate b on one wave (Params::gen_wave:
+// small batches, where k_bgen's chain of 11 pivots + 16 positions x (an
+// 11-term dot product, sqrt, divide, 11 broadcasts) on one quad is the whole
+// latency).  The same quantities in block form:
+//   A = Phi_b^-1                    symmetric sweep of Phi_b (11 pivots, a
+//                                   lane per matrix entry; -A after the sweep)
+//   V = A U,  G = 0.05 I + U^T V    fp64 MFMA (3 + 3 of 16x16x4; U = the
+//                                   block's 16 u_j as columns, features 11..
+//                                   15 zero)
+//   G = L L^T,  W = V L^-T          right-looking Cholesky of the 16 x 16 G,
+//                                   V updated alongside (16 pivots)
+// -- L_jj and w_j are k_bgen's (G_jj - sum_{i<j} L_ji^2 = 0.05 + u_j . A_j u_j
+// with A_j = A - sum_{i<j} w_i w_i^T; w_j = (A u_j - sum_{i<j} w_i L_ji) /
+// L_jj = A_j u_j / L_jj), summed in another order (fp64; ~1e-16 apart).
+// Every matrix is in the f64 MFMA accumulator layout (lane (r, h), register
+// i: row h + 4 i, column r); a pivot step publishes column k through the
+// wave's 32 doubles of LDS (xl) and every lane updates its entries.  The
+// sweep keeps A exactly symmetric (mirrored entries see the same products),
+// so register s of A is also the A operand of step s of A U.
+// 1 / d and 1 / sqrt(d) for d > 0: the hardware estimate and two Newton
+// steps (a few ulp; the pivots' chain is these few dependent operations, not
+// the IEEE divide and square root sequences)
+DEVI double rcp_nr(double d) {
+  double y = __builtin_amdgcn_rcp(d);
+  y = fma(y, fma(-d, y, 1.0), y);
+  return fma(y, fma(-d, y, 1.0), y);
+}
+DEVI double rsq_nr(double d) {
+  double y = __builtin_amdgcn_rsq(d);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const double e = fma(-(d * y), y, 1.0);
+    y = fma(0.5 * y, e, y);
+  }
+  return y;
+}
+
+// NB blocks blk0, blk0 + bstride, ... of candidate b on the calling wave, their
+// pivot chains interleaved (independent: the same bits as one block per
+// wave); blocks >= nblk compute on the last block and store nothing.  xl: the
+// wave's 32 NB doubles of LDS.
+template <int NB>
+DEVI void bgen_wave(const Params& p, int b, int blk0, int bstride, double* xl) {
+  const int M = p.M, M1 = M + 1, nblk = (M1 + 15) / 16, Pp = pos_pad(M);
+  const int lane = threadIdx.x & 63, r = lane & 15, h = lane >> 4;
+  double* gen = p.gen + size_t(b) * Pp * kGenStride;
+  double* gm = p.genm + size_t(b) * Pp;
+  int j0[NB];
+  bool live[NB];
+  d4 A[NB];
+  double U[NB][3];
+#pragma unroll
+  for (int t = 0; t < NB; ++t) {
+    const int blk = blk0 + t * bstride;
+    live[t] = blk < nblk;
+    const int bc = live[t] ? blk : nblk - 1;
+    j0[t] = bc * 16;
+    const double* Gb = p.phib + (size_t(b) * nblk + bc) * 66;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int a = h + 4 * i;
+      A[t][i] = a < 11 && r < 11 ? Gb[sym11i(min(a, 10), min(r, 10))] : 0.0;
+    }
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int f = 4 * s + h;  // feature 11 is the mean's slot: zero here
+      U[t][s] = f < 11 && j0[t] + r < M1 ? gen[gen_uplane(Pp) + size_t(j0[t] + r) * kGenRow + f] : 0.0;
+    }
+  }
+  // sweep: A_kk <- -1/d, A_ik = A_ki <- A_ik / d, A_ij <- A_ij - A_ik A_kj / d
+#pragma unroll
+  for (int k = 0; k < 11; ++k) {
+    if (r == k) {
+#pragma unroll
+      for (int t = 0; t < NB; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xl[32 * t + h + 4 * i] = A[t][i];
+    }
+    wave_sync();
+    double d[NB], cr[NB], ci[NB][4];
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+      d[t] = xl[32 * t + k];
+      cr[t] = xl[32 * t + r];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ci[t][i] = xl[32 * t + h + 4 * i];
+    }
+    wave_sync();
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+      const double id = rcp_nr(d[t]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int a = h + 4 * i;
+        A[t][i] = a == k ? (r == k ? -id : cr[t] * id) : (r == k ? ci[t][i] * id : A[t][i] - (ci[t][i] * cr[t]) * id);
+      }
+    }
+  }
+  const d4 zero = d4{0.0, 0.0, 0.0, 0.0};
+  d4 V[NB], G[NB];
+#pragma unroll
+  for (int t = 0; t < NB; ++t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) A[t][i] = -A[t][i];
+    V[t] = zero;
+    G[t] = zero;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) V[t] = mfma64(A[t][s], U[t][s], V[t]);
+#pragma unroll
+    for (int s = 0; s < 3; ++s) G[t] = mfma64(U[t][s], V[t][s], G[t]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (h + 4 * i == r) G[t][i] = G[t][i] + kRidge;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (r == k) {
+#pragma unroll
+      for (int t = 0; t < NB; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          xl[32 * t + h + 4 * i] = G[t][i];
+          xl[32 * t + 16 + h + 4 * i] = V[t][i];
+        }
+    }
+    wave_sync();
+    double d[NB], gr[NB], gi[NB][4], vi[NB][4];
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+      d[t] = xl[32 * t + k];
+      gr[t] = xl[32 * t + r];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        gi[t][i] = xl[32 * t + h + 4 * i];
+        vi[t][i] = xl[32 * t + 16 + h + 4 * i];
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+      const double rl = rsq_nr(d[t]);
+      const double lr = r > k ? gr[t] * rl : 0.0;
+      double wk[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const double li = h + 4 * i > k ? gi[t][i] * rl : 0.0;
+        wk[i] = vi[t][i] * rl;
+        G[t][i] = G[t][i] - li * lr;
+        V[t][i] = V[t][i] - wk[i] * lr;
+      }
+      if (live[t] && r == k && j0[t] + k < M1) {
+        double* g = gen + size_t(j0[t] + k) * kGenRow + kGenW;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) g[h + 4 * i] = h + 4 * i < 11 ? wk[i] : 0.0;  // whole rows: slot 11 is 0
+        if (h == 0) gm[j0[t] + k] = d[t] * rl;  // L_jj
+      }
+    }
+  }
+}
+
+constexpr int kGenWaveWaves = 4;
+__global__ __launch_bounds__(64 * kGenWaveWaves) void k_bgen_wave(Params p) {
+  __shared__ double xl[kGenWaveWaves][32];
+  const int nblk = (p.M + 1 + 15) / 16;
+  const int w = threadIdx.x >> 6, gw = blockIdx.x * kGenWaveWaves + w;
+  if (gw >= p.nb * nblk) return;  // whole waves; no workgroup barrier below
+  bgen_wave<1>(p, p.b0 + gw / nblk, gw % nblk, 0, xl[w]);
+}
+
 // k_bsigma (last beta-iteration only): sigma_best when argmin is a new
 // sample -- its sigma coordinate drawn with the NEW generators (Q4,
 // compute_beta.py:133-145): y_M = mean_M + L_MM z_M + u_M . sum_{j<M} w_j z_j
@@ -2499,10 +2695,10 @@ __global__ __launch_bounds__(64) void k_mmdfinal(Params p, int t) {
 // candidate's intermediates (samples, selections, K_red, generators) in
 // global memory that this workgroup alone touches -- L2-resident at this
 // size.  Every phase is the body of its multi-kernel counterpart (same
-// operations, so the same bits): samples by bsample_tile (a wave per tile),
+// operations, so the same bits): samples by bsample_tile_lds (a wave per tile),
 // selection by bselect_wave, kernel sums / K_red by bkernel_body, direct row
 // sums by bdirect_body, the QPs by bqp_solve (a quad each), elites by
-// belite_body, generators by bgen_quad, sigma_best by bsigma_body.
+// belite_body, generators by bgen_wave, sigma_best by bsigma_body.
 // 8 waves (512 threads): the QP and generator phases need up to 256 VGPRs.
 constexpr int kSmallWaves = 8;
 constexpr int kSmallThreads = 64 * kSmallWaves;
@@ -2513,7 +2709,11 @@ HDI size_t small_lds(int M, int n, int R) {
   const size_t k = ker_lds(M, n, ker_scratch(M, n, 1, kSmallWaves)).total;
   const size_t d = dir_lds(M, n).total, e = elite_lds(M + 1).total;
   const size_t q = size_t(kBetaSamples) * tri_stride(n) * 4;  // the QPs' K_red
+  const size_t g = size_t(kSmallWaves) * 4 * 32 * 8;             // bgen_wave<4>'s pivot columns
+  const size_t gl = gen_lds_bytes(M);                             // the sampler's generator copy
   b = b > q ? b : q;
+  b = b > g ? b : g;
+  b = b > gl ? b : gl;
   b = b > k ? b : k;
   b = b > d ? b : d;
   b = b > e ? b : e;
@@ -2529,7 +2729,15 @@ DEVI int opaque_s(int v) {
   return v;
 }
 
-template <int NQ, int R, int G, int NP, int NV4>
+// phase stamps of beta-iteration 5 (MPCMMD_STAMPW; rows 32768 + workgroup,
+// apart from the kernel-sum body's own stamps): tools/stamp_small.py
+#define SMALL_STAMP(p, slot)                                                             \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && (p).dbgw)                                                    \
+      (p).dbgw[size_t(32768 + blockIdx.x) * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
+template <int NQ, int R, int G, int NP, int NV4, int GNB>
 __global__ __launch_bounds__(kSmallThreads) void k_bcem_small(Params p0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int cand = blockIdx.x;
@@ -2545,8 +2753,20 @@ __global__ __launch_bounds__(kSmallThreads) void k_bcem_small(Params p0) {
     // samples of this iteration (compute_beta.py:51-68); the first ones are
     // the shared initial draws (Q3), taken from the handle's selection table
     if (tb > 0) {
-      if (w < kSampleTiles) bsample_tile(p, tb, b, w);
+      if (tb == 5) SMALL_STAMP(p, 0);
+      {  // the generators into LDS (W and U planes, genm), then the walkers
+        const int Pp = pos_pad(M);
+        const double2* gsrc = reinterpret_cast<const double2*>(p.gen + size_t(b) * Pp * kGenStride);
+        const double2* msrc = reinterpret_cast<const double2*>(p.genm + size_t(b) * Pp);
+        double2* dst = reinterpret_cast<double2*>(smem);
+        const int ng = Pp * kGenRow, nm = Pp >> 1;  // double2 counts
+        for (int i = tid; i < ng + nm; i += kSmallThreads) dst[i] = i < ng ? gsrc[i] : msrc[i - ng];
+        if (tid < 8) dst[ng + nm + tid] = double2{0.0, 0.0};
+      }
       __syncthreads();
+      if (w < kSampleTiles) bsample_tile_lds(p, tb, b, w, reinterpret_cast<const double*>(smem));
+      __syncthreads();
+      if (tb == 5) SMALL_STAMP(p, 1);
       char* sw = smem + size_t(w) * small_sel_bytes(R);
       unsigned long long* cand_l = reinterpret_cast<unsigned long long*>(sw);
       uint32_t* lm = reinterpret_cast<uint32_t*>(sw + size_t(64 * R + 8) * 8);
@@ -2557,9 +2777,11 @@ __global__ __launch_bounds__(kSmallThreads) void k_bcem_small(Params p0) {
       for (int e = tid; e < kBetaSamples; e += kSmallThreads) p.bsig[size_t(b) * kBetaSamples + e] = p.sig0[e];
     }
     __syncthreads();
+    if (tb == 5) SMALL_STAMP(p, 2);
     // K_mixed row sums and K_red (compute_beta.py:120-127)
     bkernel_body<kSmallWaves>(p, tb, cand, 0, 1, int(ker_scratch(M, n, tb, kSmallWaves)), smem);
     __syncthreads();
+    if (tb == 5) SMALL_STAMP(p, 3);
     if (tb > 0) {
       const int total = bdirect_total(p, b, 1);  // block-uniform
       if (total > 0) {
@@ -2567,6 +2789,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_bcem_small(Params p0) {
         __syncthreads();
       }
     }
+    if (tb == 5) SMALL_STAMP(p, 4);
     // the QPs (compute_beta.py:70-91), a quad each, the samples' K_red staged
     // in LDS (one contiguous copy: the candidate's triangles are consecutive)
     {
@@ -2582,19 +2805,19 @@ __global__ __launch_bounds__(kSmallThreads) void k_bcem_small(Params p0) {
       bqp_solve<NP>(p, b, s_lo + gc, ok, reinterpret_cast<const float*>(smem) + size_t(gc) * ntri);
     }
     __syncthreads();
+    if (tb == 5) SMALL_STAMP(p, 5);
     // elites, mean, generator level 1 (compute_beta.py:51-68, 133-157)
     belite_body(p, tb, b, smem);
     __syncthreads();
-    // generator level 2, a quad per 16-position block
+    if (tb == 5) SMALL_STAMP(p, 6);
+    // generator level 2, a wave per 16-position block
     {
       const int nblk = (M + 1 + 15) / 16;
-      for (int g0 = 0; g0 < nblk; g0 += kSmallThreads / 4) {
-        const int blk = g0 + (tid >> 2);
-        const bool live = blk < nblk;
-        bgen_quad(p, b, live ? blk : nblk - 1, live);
-      }
+      double* xl = reinterpret_cast<double*>(smem) + 32 * GNB * w;
+      for (int blk = w; blk < nblk; blk += kSmallWaves * GNB) bgen_wave<GNB>(p, b, blk, kSmallWaves, xl);
     }
     __syncthreads();
+    if (tb == 5) SMALL_STAMP(p, 7);
     if (tb == kBetaIters - 1 && p.bimin[b] >= kBetaElite) {  // block-uniform
       bsigma_body(p, tb, b, reinterpret_cast<double*>(smem));
       __syncthreads();
@@ -2625,7 +2848,7 @@ bool mmdopt_supported(int n, int H, int O, std::string* why) {
 }
 
 void launch_mother(const Params& p, int t, hipStream_t s) {
-  hipLaunchKernelGGL(k_mother, dim3(p.Bt), dim3(kThreads), size_t(2) * p.n * p.H * 4, s, p, t);
+  hipLaunchKernelGGL(k_mother, dim3(p.Bt), dim3(kThreads), size_t(3) * p.n * p.H * 4, s, p, t);
 }
 
 void launch_bdist(const Params& p, hipStream_t s) {
@@ -2783,25 +3006,32 @@ void launch_belite(const Params& p, int tb, hipStream_t s) {
 
 void launch_bgen(const Params& p, int tb, hipStream_t s) {
   const int nblk = (p.M + 1 + 15) / 16;
-  hipLaunchKernelGGL(k_bgen, dim3((p.nb * nblk * 4 + 255) / 256), dim3(256), 0, s, p);
+  if (p.gen_wave)
+    hipLaunchKernelGGL(k_bgen_wave, dim3((p.nb * nblk + kGenWaveWaves - 1) / kGenWaveWaves), dim3(64 * kGenWaveWaves), 0,
+                       s, p);
+  else
+    hipLaunchKernelGGL(k_bgen, dim3((p.nb * nblk * 4 + 255) / 256), dim3(256), 0, s, p);
   if (tb == kBetaIters - 1) hipLaunchKernelGGL(k_bsigma, dim3(p.nb), dim3(kThreads), 0, s, p, tb);
 }
 
-bool bcem_small_ok(const Params& p) { return p.n <= 24 && p.nb <= 512; }
+// (k_bcem_small's generators are bgen_wave's: handles with gen_wave only)
+bool bcem_small_ok(const Params& p) {
+  return p.gen_wave && p.n <= 24 && p.nb <= 512 && small_lds(p.M, p.n, 1) <= kLdsBudget;
+}
 
 void launch_bcem_small(const Params& p, hipStream_t s) {
   const int n = p.n, M = p.M;
   const dim3 grid(p.nb), block(kSmallThreads);
   if (M <= 64)
-    hipLaunchKernelGGL((k_bcem_small<1, 1, 32, 8, 1>), grid, block, small_lds(M, n, 1), s, p);
+    hipLaunchKernelGGL((k_bcem_small<1, 1, 32, 8, 1, 1>), grid, block, small_lds(M, n, 1), s, p);
   else if (M <= 128)
-    hipLaunchKernelGGL((k_bcem_small<2, 1, 32, 16, 1>), grid, block, small_lds(M, n, 1), s, p);
+    hipLaunchKernelGGL((k_bcem_small<2, 1, 32, 16, 1, 1>), grid, block, small_lds(M, n, 1), s, p);
   else if (M <= 256)
-    hipLaunchKernelGGL((k_bcem_small<4, 1, 32, 16, 1>), grid, block, small_lds(M, n, 1), s, p);
+    hipLaunchKernelGGL((k_bcem_small<4, 1, 32, 16, 1, 2>), grid, block, small_lds(M, n, 1), s, p);
   else if (M <= 512)
-    hipLaunchKernelGGL((k_bcem_small<8, 1, 32, 24, 2>), grid, block, small_lds(M, n, 1), s, p);
+    hipLaunchKernelGGL((k_bcem_small<8, 1, 32, 24, 2, 2>), grid, block, small_lds(M, n, 1), s, p);
   else
-    hipLaunchKernelGGL((k_bcem_small<12, 1, 32, 24, 3>), grid, block, small_lds(M, n, 1), s, p);
+    hipLaunchKernelGGL((k_bcem_small<12, 1, 32, 24, 3, 2>), grid, block, small_lds(M, n, 1), s, p);
 }
 
 void launch_mmdfinal(const Params& p, int t, hipStream_t s) {

@@ -8,15 +8,15 @@
 //                 points to Params::rxy
 //   k_frenet      global_to_frenet_trajs (cem_helper.py:206-242): every
 //                 recorded point to (s, d) by the closest of the P path points,
-//                 one thread per point, the path staged in LDS
+//                 a quad of lanes per point, the path staged in LDS
 //   k_risk_carla  per candidate: collision residual in the Frenet frame
 //                 (costs.py:48-57, a = 4.5, b = 3), lane and desired-lane bars,
 //                 then CVaR (costs.py:133-153, 84-100, 184-198) or the MMD with
 //                 the beta-CEM's beta / sigma (costs.py:116-130, 70-82, 168-181)
 //
 // Splitting the rollouts (sequential in the step) from the Frenet search
-// (independent per point) keeps the search, the dominant cost, at one thread
-// per point: B x rows x H threads instead of B x rows.
+// (independent per point) keeps the search, the dominant cost, at a quad of
+// lanes per point: B x rows x H x 4 threads instead of B x rows.
 #include "block.hpp"
 #include "frenet.hpp"
 #include "kernels.hpp"
@@ -29,61 +29,79 @@ namespace {
 
 constexpr int kN = 100;
 
+// One wave per (candidate, 64 rows).  The step's control and tan(steer) do
+// not depend on the state: every lane first computes (row, step) pairs of
+// the wave's rows into LDS (tan off the step chain, spread over the wave's
+// 64 lanes rather than the S < 64 live rows), then each row runs its chain of
+// H - 1 steps with one fp64 sincos per step.
+constexpr int kRollLds = 64 * 2 * kMaxH;  // floats: [h][row] controls and tan(steer)
 __global__ __launch_bounds__(64) void k_roll_carla(Params p, int t, int mode) {
-  const int b = blockIdx.x, S = p.S, H = p.H, n = p.n;
-  const int r = blockIdx.y * 64 + threadIdx.x;
-  if (r >= S) return;
+  __shared__ float ctl[kRollLds];
+  const int b = blockIdx.x, S = p.S, H = p.H, n = p.n, lane = threadIdx.x;
+  const int r0 = blockIdx.y * 64, rows = min(64, S - r0);
   const Cfg cf = cfg_of(p, b / p.B);
-  int m = r;  // the row's noisy initial state
-  const float *ar = nullptr, *sr = nullptr;
-  if (mode == 1) {  // reduced-set row m of the mother set: controls repeat(acc, n) x tile(steer, n)
-    m = p.bestsel[size_t(b) * n + r];
-    const float* ctrl = p.ctrl_n + size_t(b) * 2 * n * H;
-    ar = ctrl + (m / n) * H;
-    sr = ctrl + n * H + (m % n) * H;
+  float* an_l = ctl;             // [h][64]
+  float* tn_l = ctl + 64 * kMaxH;
+  const float* ctrl = p.ctrl_n + size_t(b) * 2 * n * H;
+  const float* bpl = p.noise == 1 ? p.bplane + size_t(b) * 2 * H * S : nullptr;
+  for (int e = lane; e < rows * (H - 1); e += 64) {
+    const int h = e / rows, rr = e - h * rows, r = r0 + rr;
+    float an, sn;
+    if (mode == 1) {  // reduced-set row m of the mother set: controls repeat(acc, n) x tile(steer, n)
+      const int m = p.bestsel[size_t(b) * n + r];
+      an = ctrl[(m / n) * H + h];
+      sn = ctrl[n * H + (m % n) * H + h];
+    } else {
+      noisy_control<true>(p, cf, t, r, h, p.acc[size_t(b) * kN + h], p.steer[size_t(b) * kN + h], an, sn, bpl);
+    }
+    an_l[h * 64 + rr] = an;
+    tn_l[h * 64 + rr] = float(tan(double(sn)));
   }
+  __syncthreads();
+  if (lane >= rows) return;
+  const int r = r0 + lane;
+  const int m = mode == 1 ? p.bestsel[size_t(b) * n + r] : r;  // the row's noisy initial state
   const float* st = p.st0r + (size_t(cf.g) * p.R0 + m) * 8;
   float x = st[0], y = st[1], vx = st[2], vy = st[3], psi = st[4];
   float* out = p.rxy + (size_t(b) * S + r) * 2 * H;
-  const float* bpl = p.noise == 1 ? p.bplane + size_t(b) * 2 * H * S : nullptr;
   for (int h = 0; h < H; ++h) {
     out[h] = x;  // x_roll[:, h] = state before step h (cem_helper.py:794-797)
     out[H + h] = y;
     if (h == H - 1) break;
-    float an, sn;
-    if (mode == 1) {
-      an = ar[h];
-      sn = sr[h];
-    } else {
-      noisy_control<true>(p, cf, t, r, h, p.acc[size_t(b) * kN + h], p.steer[size_t(b) * kN + h], an, sn, bpl);
-    }
-    bicycle_step_cr(x, y, vx, vy, psi, an, sn, p.wheel_base);
+    bicycle_step_cr_t(x, y, vx, vy, psi, an_l[h * 64 + lane], tn_l[h * 64 + lane], p.wheel_base);
   }
 }
 
+// four lanes per point (frenet_point_quad): B x rows x H x 4 threads, so the
+// path scan's LDS latency is hidden by ~4 waves per SIMD
 __global__ __launch_bounds__(256) void k_frenet(Params p, int total) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int P = p.P, H = p.H, S = p.S, g = blockIdx.y;
+  const int P = p.P, H = p.H, S = p.S, g = blockIdx.y, Pq = frenet_quarter(P);
   float2* pxy = reinterpret_cast<float2*>(smem);
-  float* arc = reinterpret_cast<float*>(pxy + P);
+  float* arc = reinterpret_cast<float*>(pxy + 4 * Pq);
   float* Fxd = arc + P;
   float* Fyd = Fxd + P;
   const float* pa = p.path + size_t(g) * 6 * kMaxPath;
-  for (int j = threadIdx.x; j < P; j += blockDim.x) {
-    pxy[j] = make_float2(pa[j], pa[kMaxPath + j]);
-    arc[j] = pa[2 * kMaxPath + j];
-    Fxd[j] = pa[3 * kMaxPath + j];
-    Fyd[j] = pa[4 * kMaxPath + j];
+  const float inf = __int_as_float(0x7f800000);
+  for (int j = threadIdx.x; j < 4 * Pq; j += blockDim.x) {
+    pxy[j] = j < P ? make_float2(pa[j], pa[kMaxPath + j]) : make_float2(inf, inf);
+    if (j < P) {
+      arc[j] = pa[2 * kMaxPath + j];
+      Fxd[j] = pa[3 * kMaxPath + j];
+      Fyd[j] = pa[4 * kMaxPath + j];
+    }
   }
   __syncthreads();
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;  // point of configuration g
+  const int e = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;  // point of configuration g (quad-uniform)
   if (e >= total) return;
   const int bl = e / (S * H), rh = e - bl * S * H, r = rh / H, h = rh - r * H;
   float* q = p.rxy + ((size_t(g) * p.B + bl) * S + r) * 2 * H + h;
   float s, d;
-  frenet_point(q[0], q[H], pxy, arc, Fxd, Fyd, P, s, d);
-  q[0] = s;
-  q[H] = d;
+  frenet_point_quad(q[0], q[H], pxy, arc, Fxd, Fyd, P, Pq, s, d);
+  if ((threadIdx.x & 3) == 0) {
+    q[0] = s;
+    q[H] = d;
+  }
 }
 
 size_t risk_carla_lds(int O, int H, int S) {
@@ -180,8 +198,8 @@ void launch_roll_carla(const Params& p, int t, int mode, hipStream_t s) {
 
 void launch_frenet(const Params& p, hipStream_t s) {
   const int total = p.B * p.S * p.H;
-  const size_t lds = size_t(p.P) * 20;
-  hipLaunchKernelGGL(k_frenet, dim3((total + 255) / 256, p.G), dim3(256), lds, s, p, total);
+  const size_t lds = size_t(4) * frenet_quarter(p.P) * 8 + size_t(p.P) * 12;
+  hipLaunchKernelGGL(k_frenet, dim3((total * 4 + 255) / 256, p.G), dim3(256), lds, s, p, total);
 }
 
 void launch_risk_carla(const Params& p, int t, int mode, hipStream_t s) {

@@ -742,9 +742,41 @@ __global__ __launch_bounds__(256) void k_beta_fix(Params p, int t) {
   }
 }
 
+// The CARLA variant's planes: every element through the full sampler (as
+// k_beta_fix, a quad per element) and the fp64 combine (beta_combine_cr)
+__global__ __launch_bounds__(256) void k_beta_planes_cr(Params p, int t, unsigned total) {
+  const int S = p.S, H = p.H;
+  const int lane = threadIdx.x & 63, k = lane & 3, q0 = lane & ~3;
+  const size_t sl = size_t(kGammaTabAttempts) * 4 * S * H;
+  const uint32_t streams[4] = {kStreamGammaAccA, kStreamGammaAccB, kStreamGammaSteerA, kStreamGammaSteerB};
+  const unsigned gi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi >= 4 * total) return;  // whole quads
+  const unsigned e = gi >> 2;
+  const int r = int(e % unsigned(S)), bh = int(e / unsigned(S));
+  const int h = bh % H, b = bh / H;
+  const Cfg cf = cfg_of(p, b / p.B);
+  const float fa = fabsf(p.acc[size_t(b) * 100 + h]), fs = fabsf(p.steer[size_t(b) * 100 + h]);
+  const double al[4] = {double(2.0f * fa), double(5.0f * fa), double(2.0f * fs), double(5.0f * fs)};
+  const double alpha = k == 0 ? al[0] : k == 1 ? al[1] : k == 2 ? al[2] : al[3];
+  const uint32_t stream = k == 0 ? streams[0] : k == 1 ? streams[1] : k == 2 ? streams[2] : streams[3];
+  double g, u;
+  gamma_parts_tab(mt_const(alpha), cf.gtab + size_t(k) * sl, S, H, r, h, iteration_key0(cf.idx_mpc, t), p.seed, stream,
+                  uint32_t(r) * uint32_t(H) + uint32_t(h), g, u);
+  const double g1 = __shfl(g, q0 + (k | 1), 64), u1 = __shfl(u, q0 + (k | 1), 64);  // the pair's b gamma
+  if ((k & 1) == 0) {
+    const double a = k == 0 ? al[0] : al[2], bb = k == 0 ? al[1] : al[3];
+    p.bplane[size_t(b) * 2 * H * S + (size_t(k == 0 ? 0 : H) + h) * S + r] = beta_combine_cr(a, bb, 2.0, 5.0, g, u, g1, u1);
+  }
+}
+
 }  // namespace
 
 void launch_beta_planes(const Params& p, int t, hipStream_t s) {
+  if (p.carla) {
+    const unsigned total = unsigned(p.Bt) * p.H * p.S;
+    hipLaunchKernelGGL(k_beta_planes_cr, dim3((4 * total + 255) / 256), dim3(256), 0, s, p, t, total);
+    return;
+  }
   static const bool rows = [] {  // MPCMMD_BETA_ROWS=1: the row-lane kernel (A/B)
     const char* e = std::getenv("MPCMMD_BETA_ROWS");
     return e && std::atoi(e) != 0;

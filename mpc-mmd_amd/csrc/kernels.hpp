@@ -99,6 +99,8 @@ struct Params {
   float* rbar;             // [3][Bt][S] per-row maxima (collision, lane lb, ub) of the fused rollouts
   int32_t beta_dump;       // fused rollouts also store their Beta draws in bplane (MPCMMD_BETA_DUMP, tests)
   int32_t risk_rows;       // 1 (default): the row-lane rollouts over Beta planes; 0: fused (MPCMMD_RISK_FUSED=1)
+  int32_t gen_wave;        // 1: beta-CEM generators by k_bgen_wave (a wave per block: the latency-bound small
+                           // batches, Bt <= 512); 0: k_bgen (a quad per block: throughput). Fixed per handle.
   const float* beta_z0;    // [100][M+1]
   const float* beta_z;     // [20][pos_pad(M) * kBzCols] fp32 normals (bz_index layout, zero padded)
   // carry / state

@@ -717,6 +717,11 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     if (const char* g = std::getenv("MPCMMD_GRAPH")) h->graphs = std::atoi(g) != 0;
     if (const char* g = std::getenv("MPCMMD_AHEAD")) h->ahead_on = std::atoi(g) != 0;
     if (const char* g = std::getenv("MPCMMD_FUSED")) h->fused_small = std::atoi(g) != 0;
+    // the generators' variant is a property of the handle (its capacity), not
+    // of a launch's candidate group: a candidate's bits do not depend on how
+    // the batch is split into groups or whether k_bcem_small runs it
+    p.gen_wave = BT <= 512 && h->n <= 24;
+    if (const char* g = std::getenv("MPCMMD_GENWAVE")) p.gen_wave = std::atoi(g) != 0;
     if (const char* g = std::getenv("MPCMMD_BETA_DUMP")) p.beta_dump = std::atoi(g) != 0;
     p.risk_rows = 1;  // the row-lane path is the faster one at configs[2]; MPCMMD_RISK_FUSED=1: fused
     if (const char* g = std::getenv("MPCMMD_RISK_FUSED")) p.risk_rows = std::atoi(g) == 0;

@@ -206,18 +206,44 @@ DEVI float beta_combine(double a, double b, double ra, double rb, double ga, dou
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(d));
 }
 
+// beta_combine in fp64, rounded once (the CARLA variant, Params::carla):
+// oracle/rng.py:beta_draws' formula -- G = G' exp(log U / alpha) and Ga / (Ga
+// + Gb) while both boost exponents exceed -600, else the same ratio in log
+// space -- so a draw is the oracle's float32 value but where the two fp64
+// evaluations straddle a float32 rounding boundary.  The CARLA risk takes
+// the closest path point of every rollout point (a discontinuous map): a
+// draw a few ulp off moves a candidate's risk by a path step, where the
+// static variant's risks move by ulps.
+constexpr double kBoostLinMin = -600.0;
+DEVI float beta_combine_cr(double a, double b, double ra, double rb, double ga, double ua, double gb, double ub) {
+  if (a == 0.0 && b == 0.0) return (ua * rb > ub * ra) ? 1.0f : 0.0f;
+  const double ba = a < 1.0 ? ua / (a > 0.0 ? a : 1.0) : 0.0;
+  const double bb = b < 1.0 ? ub / (b > 0.0 ? b : 1.0) : 0.0;
+  double out;
+  if (ba > kBoostLinMin && bb > kBoostLinMin) {
+    const double Ga = ga * (a < 1.0 ? exp(ba) : 1.0), Gb = gb * (b < 1.0 ? exp(bb) : 1.0);
+    out = Ga / (Ga + Gb);
+  } else {
+    const double la = log(ga) + ba, lb = log(gb) + bb, lm = la > lb ? la : lb;
+    const double ea = exp(la - lm), eb = exp(lb - lm);
+    out = ea / (ea + eb);
+  }
+  return float(out);
+}
+
 // Beta(a, b) with a = ra*s, b = rb*s (s = |control|); s == 0 takes the
 // alpha -> 0+ limit (oracle/rng.py:beta_draws, DESIGN.md Numerics).  tab_a,
 // tab_b: the attempt-table slices of the two gamma streams.
 // mc_a, mc_b: mt_const(a), mt_const(b) (shared by every row r of a step).
+// cr: the fp64 combine (beta_combine_cr, the CARLA variant).
 DEVI float beta_draw_tab(double a, double b, double ra, double rb, MtConst mc_a, MtConst mc_b,
                          const double* tab_a, const double* tab_b, int S, int H, int r, int h, uint32_t k0,
-                         uint32_t k1, uint32_t stream_a, uint32_t stream_b) {
+                         uint32_t k1, uint32_t stream_a, uint32_t stream_b, bool cr = false) {
   const uint32_t elem = uint32_t(r) * uint32_t(H) + uint32_t(h);
   double ga, ua, gb, ub;
   gamma_parts_tab(mc_a, tab_a, S, H, r, h, k0, k1, stream_a, elem, ga, ua);
   gamma_parts_tab(mc_b, tab_b, S, H, r, h, k0, k1, stream_b, elem, gb, ub);
-  return beta_combine(a, b, ra, rb, ga, ua, gb, ub);
+  return cr ? beta_combine_cr(a, b, ra, rb, ga, ua, gb, ub) : beta_combine(a, b, ra, rb, ga, ua, gb, ub);
 }
 
 // Table-only path for the hot plane kernel: attempts k0 .. kGammaTabAttempts

@@ -28,9 +28,9 @@ DEVI void beta_pair(const Params& p, const Cfg& cf, int t, int r, int h, float a
     m[0] = mt_const(aa), m[1] = mt_const(ab), m[2] = mt_const(sa), m[3] = mt_const(sb);
   }
   nba = beta_draw_tab(aa, ab, 2.0, 5.0, m[0], m[1], cf.gtab, cf.gtab + sl, S, H, r, h, k0, k1, kStreamGammaAccA,
-                      kStreamGammaAccB);
+                      kStreamGammaAccB, p.carla != 0);
   nbs = beta_draw_tab(sa, sb, 2.0, 5.0, m[2], m[3], cf.gtab + 2 * sl, cf.gtab + 3 * sl, S, H, r, h, k0, k1,
-                      kStreamGammaSteerA, kStreamGammaSteerB);
+                      kStreamGammaSteerA, kStreamGammaSteerB, p.carla != 0);
 }
 
 // Noisy controls of noise row r at step h of outer iteration t
@@ -99,13 +99,18 @@ DEVI void bicycle_step(float& x, float& y, float& vx, float& vy, float& psi, flo
 // base 2.875, true division, tan / cos / sin evaluated in fp64 and rounded
 // once (oracle/carla.py: rollout_cr), so rollouts - and the Frenet argmins
 // taken on them - are reproducible bit for bit.
-DEVI void bicycle_step_cr(float& x, float& y, float& vx, float& vy, float& psi, float an, float sn, float wb) {
+// Here with tn = float(tan(double(steer))) computed by the caller (it does
+// not depend on the state: off the step chain), cos / sin from one fp64
+// sincos (OCML: one argument reduction, the values of cos and sin).
+DEVI void bicycle_step_cr_t(float& x, float& y, float& vx, float& vy, float& psi, float an, float tn, float wb) {
   float v = sqrtf(vx * vx + vy * vy);
   v = v + an * kDt;
-  const float psidot = (v * float(tan(double(sn)))) / wb;
+  const float psidot = (v * tn) / wb;
   psi = psi + psidot * kDt;
-  vx = v * float(cos(double(psi)));
-  vy = v * float(sin(double(psi)));
+  double sp, cp;
+  sincos(double(psi), &sp, &cp);
+  vx = v * float(cp);
+  vy = v * float(sp);
   x = x + vx * kDt;
   y = y + vy * kDt;
 }
