@@ -477,6 +477,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--profile-steps", type=int, default=20)
     ap.add_argument("--extra", type=int, default=1, help="N = 1: also time the other BASELINE workloads (0 = skip)")
+    ap.add_argument("--carla-n", type=int, default=10, help="--workload carla: num_reduced_set (10 or 22)")
     a = ap.parse_args()
 
     import torch
@@ -489,7 +490,7 @@ def main():
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world} (launch N>1 with torchrun)")
     torch.cuda.set_device(local)
     if a.workload == "carla":  # configs[4] alone (one GPU, a real-time tick loop: no sharding)
-        print(json.dumps({"metric": "CARLA ticks/s (mmd_opt + cvar per tick)", **run_carla(a.steps, a.warmup, local)}),
+        print(json.dumps({"metric": "CARLA ticks/s (mmd_opt + cvar per tick)", **run_carla(a.steps, a.warmup, local, n=a.carla_n)}),
               flush=True)
         return
     if world > 1:

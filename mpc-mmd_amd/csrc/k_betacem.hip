@@ -41,6 +41,21 @@ namespace mpcmmd {
 
 namespace {
 
+// The thread's index.  The small-batch fused kernel (k_bcem_small.hip, which
+// compiles this file with MPCMMD_FUSED_TU) runs every phase inside one loop
+// over the beta-iterations; there each read is opaque, so nothing computed
+// from the index is hoisted out of the loop and held in registers across the
+// other phases (spills).  The per-iteration kernels read threadIdx.x.
+#ifdef MPCMMD_FUSED_TU
+DEVI unsigned tidx() {
+  unsigned t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+#else
+DEVI unsigned tidx() { return threadIdx.x; }
+#endif
+
 constexpr int kF = 22;                               // features: cx (11) | cy (11)
 constexpr int kNew = kBetaSamples - kBetaElite;      // 89 resampled rows per iteration
 constexpr int kThreads = 512;
@@ -88,6 +103,7 @@ DEVI float kred_perturb(float v, int e) {
 
 // ------------------------------------------------------------------------
 // k_mother
+#ifndef MPCMMD_FUSED_TU
 __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = p.n, H = p.H, M = p.M, b = blockIdx.x;
@@ -96,7 +112,7 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
   float* sn = an + n * H;
   float* tn = sn + n * H;  // CARLA: float(tan(double(steer))) of each control, off the rows' step chains
   float* gctrl = p.ctrl_n + size_t(b) * 2 * n * H;
-  for (int idx = threadIdx.x; idx < n * H; idx += blockDim.x) {
+  for (int idx = tidx(); idx < n * H; idx += blockDim.x) {
     const int r = idx / H, h = idx % H;
     float a, s;
     noisy_control(p, cf, t, r, h, p.acc[size_t(b) * 100 + h], p.steer[size_t(b) * 100 + h], a, s);
@@ -108,7 +124,7 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
   }
   __syncthreads();
   float* F = p.feat + size_t(b) * kF * M;
-  for (int m = threadIdx.x; m < M; m += blockDim.x) {
+  for (int m = tidx(); m < M; m += blockDim.x) {
     // jnp.repeat(acc, n, 0) / jnp.tile(steer, (n, 1)) (cem_helper.py:510-511)
     const float* ar = an + (m / n) * H;
     const float* sr = sn + (m % n) * H;
@@ -146,6 +162,7 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
     for (int q = 0; q < kFeatStride / 4; ++q) Fr[q] = make_float4(fr[4 * q], fr[4 * q + 1], fr[4 * q + 2], fr[4 * q + 3]);
   }
 }
+#endif
 
 // ------------------------------------------------------------------------
 // k_bdist: the L1 distance matrix of the mother features,
@@ -175,6 +192,7 @@ constexpr int kXcds = 8;
 // lanes per row) instead of 16 bytes to 64 rows.
 constexpr int kMirrorPitch = kDistRows + 4;  // floats per staged row (16-byte aligned, spreads banks)
 
+#ifndef MPCMMD_FUSED_TU
 __global__ __launch_bounds__(kDistThreads) void k_bdist(Params p) {
   __shared__ __attribute__((aligned(16))) float Fr[kDistRows][kF + 2];
   __shared__ __attribute__((aligned(16))) float Tm[kDistThreads * kMirrorPitch];
@@ -182,7 +200,7 @@ __global__ __launch_bounds__(kDistThreads) void k_bdist(Params p) {
   const int L = blockIdx.x, q = L / kXcds;
   const int b = (q / T) * kXcds + L % kXcds, r0 = (q % T) * kDistRows;
   if (b >= p.Bt) return;
-  const int tid = threadIdx.x;
+  const int tid = tidx();
   const float* Fg = p.feat + size_t(b) * kF * M;
   for (int i = tid; i < kDistRows * kF; i += kDistThreads) {
     const int r = i / kF, f = i - r * kF;
@@ -228,6 +246,7 @@ __global__ __launch_bounds__(kDistThreads) void k_bdist(Params p) {
     __syncthreads();
   }
 }
+#endif
 
 // ------------------------------------------------------------------------
 // k_bmoment: the series record of every distance row (once per outer
@@ -258,7 +277,7 @@ constexpr float kNegLog2eRow = -1.44269504088896340736f;   // == kNegLog2e
 // the lane bit the pairing flips, then the quad), ~35 VALU for all 16 totals
 // instead of a 7-step reduction per value.
 DEVI float wave_totals16(const float (&v)[16]) {
-  const int lane = threadIdx.x & 63;
+  const int lane = tidx() & 63;
   float w[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {  // lanes < 32 keep values 0..7, lanes >= 32 values 8..15
@@ -295,7 +314,7 @@ struct RowPairs {
 };
 
 DEVI RowPairs load_row_pairs(const Params& p, int r) {
-  const int lane = threadIdx.x & 63;
+  const int lane = tidx() & 63;
   RowPairs rp;
   rp.q0 = p.rp0[r];
   rp.q1 = p.rp0[r + 1];
@@ -305,7 +324,7 @@ DEVI RowPairs load_row_pairs(const Params& p, int r) {
 
 template <int NV4>
 DEVI void bmoment_row(const Params& p, int gw, const float4 (&x)[NV4], const RowPairs& rq) {
-  const int lane = threadIdx.x & 63;
+  const int lane = tidx() & 63;
   const int M = p.M;
   const int b = gw / M, r = gw - b * M;
   // columns j = 4 (lane + 64 t) + c; pad columns j >= M
@@ -384,12 +403,13 @@ DEVI void bmoment_row(const Params& p, int gw, const float4 (&x)[NV4], const Row
 template <int NV4>
 constexpr int mom_rows_per_wave() { return NV4 <= 2 ? 4 : (NV4 <= 4 ? 2 : 1); }
 
+#ifndef MPCMMD_FUSED_TU
 template <int NV4>
 __global__ __launch_bounds__(64 * kMomRowsPerBlock) void k_bmoment(Params p) {
   constexpr int RPW = mom_rows_per_wave<NV4>();
-  const int lane = threadIdx.x & 63;
+  const int lane = tidx() & 63;
   const int total = p.Bt * p.M, Md = dist_stride(p.M);
-  const int g0 = (blockIdx.x * kMomRowsPerBlock + (threadIdx.x >> 6)) * RPW;
+  const int g0 = (blockIdx.x * kMomRowsPerBlock + (tidx() >> 6)) * RPW;
   if (g0 >= total) return;  // wave-uniform
   auto load = [&](float4 (&x)[NV4], int g) {
     const float4* row = reinterpret_cast<const float4*>(p.bdist + size_t(g) * Md) + lane;  // rows of all candidates are consecutive
@@ -417,6 +437,7 @@ __global__ __launch_bounds__(64 * kMomRowsPerBlock) void k_bmoment(Params p) {
     }
   }
 }
+#endif
 
 // ------------------------------------------------------------------------
 // top-n of |v_j| (j < M) in jnp.argsort order, one wave.  out[k] (k < n) are
@@ -430,7 +451,7 @@ __global__ __launch_bounds__(64 * kMomRowsPerBlock) void k_bmoment(Params p) {
 // indices.  scratch: 2 * 64 ints of LDS owned by the wave.
 template <int NQ, class V>
 DEVI void load_keys(V val, int M, uint32_t* key) {
-  const int lane = threadIdx.x & 63;
+  const int lane = tidx() & 63;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     const int j = lane + 64 * q;
@@ -486,7 +507,7 @@ DEVI void find_thresholds(const uint32_t (*key)[NQ], int nb, int n, uint32_t* T,
 // threshold go to the largest indices.
 template <int NQ>
 DEVI void emit_top(const uint32_t* key, uint32_t T, bool exact, int n, int32_t* out, int* scratch) {
-  const int lane = threadIdx.x & 63;
+  const int lane = tidx() & 63;
   int need = 0;
   unsigned long long eqm[NQ];
   if (!exact) {
@@ -543,7 +564,7 @@ DEVI void emit_top(const uint32_t* key, uint32_t T, bool exact, int n, int32_t* 
 template <int NQ, int R>
 DEVI bool emit_window(const uint32_t* key, uint32_t T, int n, int32_t* out, unsigned long long* cand) {
   constexpr int cap = 64 * R;
-  const int lane = threadIdx.x & 63;
+  const int lane = tidx() & 63;
   const unsigned long long below = (1ull << lane) - 1ull;
   int c = 0;
 #pragma unroll
@@ -605,7 +626,7 @@ DEVI uint32_t wave_min_u32(uint32_t v) {
 // the pick by a wave minimum; lm: G words of the wave's LDS.
 template <int NQ, int G>
 DEVI uint32_t group_max_threshold(const uint32_t* key, int n, uint32_t* lm) {
-  const int lane = threadIdx.x & 63;
+  const int lane = tidx() & 63;
   uint32_t m = key[0];
 #pragma unroll
   for (int q = 1; q < NQ; ++q) m = max(m, key[q]);
@@ -656,9 +677,10 @@ DEVI void select_walk(Row row, Out out, int first, int last, int stride, int M, 
 // The first beta-iteration's selection from the handle's table (Params::sel0,
 // sig0: k_bselect's output for the shared initial samples, computed once per
 // table) into every candidate's bsel / bsig.
+#ifndef MPCMMD_FUSED_TU
 __global__ __launch_bounds__(256) void k_bsel0(Params p) {
   const int n = p.n, per = kBetaSamples * n + kBetaSamples;
-  for (size_t x = size_t(blockIdx.x) * 256 + threadIdx.x; x < size_t(p.nb) * per; x += size_t(gridDim.x) * 256) {
+  for (size_t x = size_t(blockIdx.x) * 256 + tidx(); x < size_t(p.nb) * per; x += size_t(gridDim.x) * 256) {
     const int c = int(x / per), e = int(x - size_t(c) * per), b = p.b0 + c;
     if (e < kBetaSamples * n)
       p.bsel[size_t(b) * kBetaSamples * n + e] = p.sel0[e];
@@ -666,6 +688,7 @@ __global__ __launch_bounds__(256) void k_bsel0(Params p) {
       p.bsig[size_t(b) * kBetaSamples + e - kBetaSamples * n] = p.sig0[e - kBetaSamples * n];
   }
 }
+#endif
 
 // ------------------------------------------------------------------------
 // k_bsample: the new samples of beta-CEM iteration tb >= 1 (rows 11..99,
@@ -914,10 +937,11 @@ DEVI void fold_chunk(d4& Sp, d4& S) {
   S = d4{0.0, 0.0, 0.0, 0.0};
 }
 
+#ifndef MPCMMD_FUSED_TU
 template <int TPW>
 __global__ __launch_bounds__(64 * sample_waves<TPW>()) void k_bsample(Params p, int tb) {
   const int b = p.b0 + blockIdx.x, M = p.M, Pp = pos_pad(M);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = tidx() & 63, w = tidx() >> 6;
   const int r = lane & 15, h = lane >> 4;
   const int s0 = w * TPW * 16;
   MPCMMD_STAMP(p, 0);
@@ -975,16 +999,18 @@ __global__ __launch_bounds__(64 * sample_waves<TPW>()) void k_bsample(Params p, 
   store(Yb, Pp - 16);
   MPCMMD_STAMP(p, 1);
 }
+#endif
 
 // k_bsample_chunks: the samples of k_bsample for small batches, workgroup =
 // (candidate, tile of 16 samples), one wave per chunk of blocks.  Phase 1:
 // each wave but the last sums W^T Z over its chunk (the MFMAs of the walker's
 // S_loc, from zero) into LDS; phase 2: S_pre = the earlier chunks' sums in
 // order (the walker's folds), then the chunk's blocks as in k_bsample.
+#ifndef MPCMMD_FUSED_TU
 __global__ __launch_bounds__(64 * kChunkWavesMax) void k_bsample_chunks(Params p, int tb) {
   __shared__ double dS[kChunkWavesMax - 1][3][64];
   const int b = p.b0 + blockIdx.x, M = p.M, Pp = pos_pad(M), nblk = Pp >> 4;
-  const int lane = threadIdx.x & 63, k = threadIdx.x >> 6, P = blockDim.x >> 6;
+  const int lane = tidx() & 63, k = tidx() >> 6, P = blockDim.x >> 6;
   const int r = lane & 15, h = lane >> 4, s0 = blockIdx.y * 16;
   const int cl = sample_chunk(nblk), c0 = k * cl, c1 = min(nblk, c0 + cl);
   MPCMMD_STAMP(p, 0);
@@ -1046,6 +1072,7 @@ __global__ __launch_bounds__(64 * kChunkWavesMax) void k_bsample_chunks(Params p
   block_store<1>(Yb, plane, pend - 16, M, ys, s0, r, h);
   MPCMMD_STAMP(p, 1);
 }
+#endif
 
 // One tile of 16 samples of candidate b, every block walked by the calling
 // wave: k_bsample's walker with one tile per wave, its chunk folds included
@@ -1058,7 +1085,7 @@ constexpr int kZAhead = 4;
 HDI size_t gen_lds_bytes(int M) { return size_t(pos_pad(M)) * (2 * kGenRow + 1) * 8 + 16 * 8; }  // + wA's overreach
 DEVI void bsample_tile_lds(const Params& p, int tb, int b, int tile, const double* lg) {
   const int M = p.M, Pp = pos_pad(M), nblk = Pp >> 4, cl = sample_chunk(nblk);
-  const int lane = threadIdx.x & 63, r = lane & 15, h = lane >> 4, s0 = tile * 16;
+  const int lane = tidx() & 63, r = lane & 15, h = lane >> 4, s0 = tile * 16;
   const double* LW = lg;
   const double* LU = lg + gen_uplane(Pp);
   const double* LL = lg + 2 * gen_uplane(Pp);
@@ -1137,13 +1164,14 @@ DEVI void bselect_wave(const Params& p, int tb, int b, int g, int W, unsigned lo
   const int s_lo = first_sample(tb);
   if (s_lo + g >= kBetaSamples) return;
   select_walk<NQ, R, G>(row, [&](int s) { return sel + s * n; }, s_lo + g, kBetaSamples, W, M, n, cand, lm, scratch);
-  const int lane = threadIdx.x & 63;
+  const int lane = tidx() & 63;
   for (int s = s_lo + g + lane * W; lane < 16 && s < kBetaSamples; s += 16 * W) {
     const float v = row(s)(M);
     sig[s] = tb == 0 ? fmaxf(v, 0.01f) : v;  // later rows are clipped when written
   }
 }
 
+#ifndef MPCMMD_FUSED_TU
 template <int NQ, int R, int G>
 __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
   __shared__ __attribute__((aligned(16))) unsigned long long cand[64 * R + 8];
@@ -1151,6 +1179,7 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
   __shared__ int scratch[128];
   bselect_wave<NQ, R, G>(p, tb, p.b0 + blockIdx.x, blockIdx.y, gridDim.y, cand, lm, scratch);
 }
+#endif
 
 // ------------------------------------------------------------------------
 // k_bkernel + k_bdirect: kernel_computation.py:19-65 / compute_beta.py:120-127
@@ -1272,7 +1301,7 @@ DEVI float dpp_f_ror8(float v) { return __int_as_float(dpp_i<0x128>(__float_as_i
 // v[j] per lane -> lanes 8 j + 4..7 hold the 64-lane sum of v[j] (row_ror:4
 // moves lane i - 4 into lane i, so the 8-lane group's total lands in its upper quad)
 DEVI float transpose_sum8(const float (&v)[8]) {
-  const int lane = threadIdx.x & 63;
+  const int lane = tidx() & 63;
   float a[4], c2[2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {  // lanes 0-31: slots 0..3, lanes 32-63: slots 4..7
@@ -1319,7 +1348,7 @@ DEVI void bkernel_body(const Params& p, int tb, int cand, int part, int split, i
   constexpr int kKerWaves = NW;
   constexpr int NT = 64 * kKerWaves, Q = kFeatStride / 4;
   const int b = p.b0 + cand, M = p.M, n = p.n;
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = tidx(), lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const KerLds C = ker_lds(M, n, size_t(scratch));
   short* sl = reinterpret_cast<short*>(smem + C.sel);
@@ -1471,34 +1500,36 @@ DEVI void bkernel_body(const Params& p, int tb, int cand, int part, int split, i
     }
     __syncthreads();
     MPCMMD_STAMPW(p, 3);
-    // a wave per sample of this part, all its lookups in flight together
-    // (entries lane + 64 j, j < kJ covers n <= 23; larger n loop)
+    // the (sample, entry) items of this part's samples spread over every
+    // thread, kJ items per thread in flight together (a wave per sample left
+    // most lanes idle at small n: 45 entries at n = 10)
     constexpr int kJ = 4;
-    for (int s = s_lo + part + split * w; s < kBetaSamples; s += split * kKerWaves) {
-      const short* su = sl + s * n;
-      const float cs = csg[s];
-      float* kr = kbase + size_t(s) * ntri;
-      for (int e0 = 0; e0 < nent; e0 += 64 * kJ) {
-        int t[kJ];
+    const int ns = (kBetaSamples - s_lo - part + split - 1) / split, nitems = ns * nent;
+    for (int i0 = tid; i0 < nitems; i0 += NT * kJ) {
+      int s[kJ], e[kJ], t[kJ];
 #pragma unroll
-        for (int j = 0; j < kJ; ++j) t[j] = tri[min(e0 + lane + 64 * j, nent - 1)];
-        int u0[kJ], u1[kJ];
-#pragma unroll
-        for (int j = 0; j < kJ; ++j) {
-          u0[j] = su[t[j] & 0xFF];
-          u1[j] = su[t[j] >> 8];
-        }
-        float dv[kJ];
-#pragma unroll
-        for (int j = 0; j < kJ; ++j) {
-          const int hi = max(u0[j], u1[j]), lo = min(u0[j], u1[j]);
-          dv[j] = T[hi * (hi - 1) / 2 + lo];
-        }
-#pragma unroll
-        for (int j = 0; j < kJ; ++j)
-          if (e0 + lane + 64 * j < nent)
-            kr[e0 + lane + 64 * j] = kred_perturb(__builtin_amdgcn_exp2f(dv[j] * cs), e0 + lane + 64 * j);
+      for (int j = 0; j < kJ; ++j) {
+        const int i = min(i0 + NT * j, nitems - 1), sj = i / nent;
+        s[j] = s_lo + part + split * sj;
+        e[j] = i - sj * nent;
+        t[j] = tri[e[j]];
       }
+      int u0[kJ], u1[kJ];
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) {
+        u0[j] = sl[s[j] * n + (t[j] & 0xFF)];
+        u1[j] = sl[s[j] * n + (t[j] >> 8)];
+      }
+      float dv[kJ];
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) {
+        const int hi = max(u0[j], u1[j]), lo = min(u0[j], u1[j]);
+        dv[j] = T[hi * (hi - 1) / 2 + lo];
+      }
+#pragma unroll
+      for (int j = 0; j < kJ; ++j)
+        if (i0 + NT * j < nitems)
+          kbase[size_t(s[j]) * ntri + e[j]] = kred_perturb(__builtin_amdgcn_exp2f(dv[j] * csg[s[j]]), e[j]);
     }
   } else {
     // per-sample: the union records are dead, sl holds union ranks (urow maps back)
@@ -1538,11 +1569,13 @@ DEVI void bkernel_body(const Params& p, int tb, int cand, int part, int split, i
 
 // two workgroups per CU: 8 waves per SIMD, which needs <= 64 VGPRs and <= 80
 // SGPRs (MI355X_MICROARCH.md residency rules: 90 SGPRs admitted one)
+#ifndef MPCMMD_FUSED_TU
 __global__ __launch_bounds__(64 * kKerWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_bkernel(Params p, int tb, int split, int scratch) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int cand = blockIdx.x / split, part = blockIdx.x - cand * split;
   bkernel_body<kKerWaves>(p, tb, cand, part, split, scratch, smem);
 }
+#endif
 
 // flagged pairs of candidate b (k_bkernel's parts): k_bdirect's work
 DEVI int bdirect_total(const Params& p, int b, int kparts) {
@@ -1559,7 +1592,7 @@ DEVI void bdirect_body(const Params& p, int tb, int split, int lpt, int cand, in
   constexpr bool kPrefetch = NV4 <= 4;
   constexpr int NT = 64 * kDirWaves;
   const int b = p.b0 + cand, M = p.M, n = p.n, Md = dist_stride(M);
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = tidx(), lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const DirLds C = dir_lds(M, n);
   short* sl = reinterpret_cast<short*>(smem + C.sel);
@@ -1740,6 +1773,7 @@ DEVI void bdirect_body(const Params& p, int tb, int split, int lpt, int cand, in
   MPCMMD_STAMP(p, 20);
 }
 
+#ifndef MPCMMD_FUSED_TU
 template <int NV4>
 __global__ __launch_bounds__(64 * kDirWaves) void k_bdirect(Params p, int tb, int kparts, int split, int lpt) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1748,6 +1782,7 @@ __global__ __launch_bounds__(64 * kDirWaves) void k_bdirect(Params p, int tb, in
   if (total == 0) return;  // block-uniform
   bdirect_body<NV4, kDirWaves>(p, tb, split, lpt, cand, part, total, smem);
 }
+#endif
 
 // ------------------------------------------------------------------------
 // k_bqp: compute_beta_reduced (compute_beta.py:70-91) for every sample:
@@ -1816,7 +1851,7 @@ DEVI void bqp_stage(const Params& p, int tb, float* kl) {
       float4 v[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const int i = min(i0 + int(threadIdx.x) + u * int(blockDim.x), nq * n4 - 1);
+        const int i = min(i0 + int(tidx()) + u * int(blockDim.x), nq * n4 - 1);
         const int j = i / n4, g = min(q0 + j, total - 1);
         const float4* src = reinterpret_cast<const float4*>(
             p.bkred + (size_t(p.b0 + g / per) * kBetaSamples + s_lo + g % per) * ntri);
@@ -1824,7 +1859,7 @@ DEVI void bqp_stage(const Params& p, int tb, float* kl) {
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const int i = i0 + int(threadIdx.x) + u * int(blockDim.x);
+        const int i = i0 + int(tidx()) + u * int(blockDim.x);
         if (i < nq * n4) kl4[i] = v[u];
       }
     }
@@ -1832,13 +1867,13 @@ DEVI void bqp_stage(const Params& p, int tb, float* kl) {
   }
 }
 
-// QP of sample s of candidate b on the calling quad (lane q = threadIdx.x & 3),
+// QP of sample s of candidate b on the calling quad (lane q = tidx() & 3),
 // its K_red strict lower triangle at kr (LDS staging or global); ok = false:
 // compute on the clamped inputs, store nothing
 template <int NP>
 DEVI void bqp_solve(const Params& p, int b, int s, bool ok, const float* kr) {
   constexpr int T4 = NP / 4;
-  const int n = p.n, M = p.M, q = threadIdx.x & 3;
+  const int n = p.n, M = p.M, q = tidx() & 3;
   const float* br = p.brow + (size_t(b) * kBetaSamples + s) * n;
   const double inv_m = double(1.0f / float(M));
   const float cdiag = 1.0f + 0.05f;
@@ -1987,24 +2022,32 @@ DEVI void bqp_solve(const Params& p, int b, int s, bool ok, const float* kr) {
 template <int NP>
 DEVI void bqp_quad(const Params& p, int tb, float* kl) {
   const int s_lo = first_sample(tb), per = kBetaSamples - s_lo;
-  const int gq = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  const int gq = (blockIdx.x * blockDim.x + tidx()) >> 2;
   const bool ok = gq < p.nb * per;
   const int gqc = ok ? gq : 0;
   const int b = p.b0 + gqc / per, s = s_lo + gqc % per;
   bqp_stage(p, tb, kl);
-  bqp_solve<NP>(p, b, s, ok, kl + (threadIdx.x >> 2) * tri_stride(p.n));
+  bqp_solve<NP>(p, b, s, ok, kl + (tidx() >> 2) * tri_stride(p.n));
 }
 
-HDI int qp_np(int n) { return n <= 8 ? 8 : (n <= 16 ? 16 : (n <= 24 ? 24 : (n <= 32 ? 32 : (n <= 48 ? 48 : 64)))); }
+// padded QP size (a multiple of 4: rows 4 t + q on quad lane q).  The
+// padding rows are identity rows with zero right-hand sides, whose every
+// contribution to the real rows is an exact zero: any NP >= n gives the same
+// bits
+HDI int qp_np(int n) {
+  return n <= 8 ? 8 : (n <= 12 ? 12 : (n <= 16 ? 16 : (n <= 24 ? 24 : (n <= 32 ? 32 : (n <= 48 ? 48 : 64)))));
+}
 // threads per workgroup: 32 QPs (their K_red in LDS: 30 KB at n = 22), 16 QPs
 // for n > 24 (32 KB at n = 32, so the LDS still admits 4 workgroups per CU)
 HDI_CONST int qp_threads(int np) { return np > 24 ? 64 : 128; }
 
+#ifndef MPCMMD_FUSED_TU
 template <int NP>
 __global__ __launch_bounds__(qp_threads(NP), NP == 24 ? 3 : (NP <= 16 ? 4 : 2)) void k_bqp(Params p, int tb) {
   extern __shared__ __attribute__((aligned(16))) float kl[];
   bqp_quad<NP>(p, tb, kl);
 }
+#endif
 
 // k_bqp_wave: the same QP for 32 < n <= 64, one wave per QP, lane i owns
 // row i of C (NP floats in registers).  Right-looking Cholesky with the
@@ -2015,12 +2058,13 @@ __global__ __launch_bounds__(qp_threads(NP), NP == 24 ? 3 : (NP <= 16 ? 4 : 2)) 
 // one backward solve (column sums as wave reductions).  fp32 like the quad
 // kernel; the cost beta^T K beta - 2 g^T beta in fp64 on the fp32 beta with
 // K_red re-read.
+#ifndef MPCMMD_FUSED_TU
 template <int NP>
 __global__ __launch_bounds__(256) void k_bqp_wave(Params p, int tb) {
-  const int lane = threadIdx.x & 63;
+  const int lane = tidx() & 63;
   const int n = p.n, M = p.M;
   const int s_lo = first_sample(tb), per = kBetaSamples - s_lo;
-  const int gq = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int gq = blockIdx.x * 4 + (tidx() >> 6);
   if (gq >= p.nb * per) return;  // whole waves
   const int b = p.b0 + gq / per, s = s_lo + gq % per;
   const int ntri = tri_stride(n);
@@ -2090,6 +2134,7 @@ __global__ __launch_bounds__(256) void k_bqp_wave(Params p, int tb) {
   if (real) bt[lane] = bf;
   if (lane == 0) p.bcost[size_t(b) * kBetaSamples + s] = float(c1 - 2.0 * c3);
 }
+#endif
 
 // ------------------------------------------------------------------------
 // k_belite: elites, mean, next generators; on the last iteration the outputs
@@ -2102,24 +2147,24 @@ struct EliteLds {
   size_t Gb, misc, carry, ublk, total;
 };
 constexpr int kUPitch = 12;  // doubles per position row of the per-wave u staging
-HDI EliteLds elite_lds(int M1) {
+HDI EliteLds elite_lds(int M1, int waves = kThreads / 64) {
   EliteLds L{};
   const int nblk = (M1 + 15) / 16;
   L.Gb = 0;
   L.misc = (size_t(nblk) * 66 * 8 + 15) & ~size_t(15);
   L.carry = L.misc + 1024;
   L.ublk = (L.carry + size_t(kBetaElite) * (2 * kMaxReduced + 2) * 4 + 15) & ~size_t(15);
-  L.total = L.ublk + size_t(kThreads / 64) * 16 * kUPitch * 8;  // one 16-position block per wave
+  L.total = L.ublk + size_t(waves) * 16 * kUPitch * 8;  // one 16-position block per wave
   return L;
 }
 
 // packed upper index of (a <= c) in an 11 x 11 symmetric matrix
 HDI int sym11(int a, int c) { return a * 11 - a * (a - 1) / 2 + (c - a); }
 
-// The body of k_belite for candidate b (kThreads threads)
+// The body of k_belite for candidate b (any whole number of waves)
 DEVI void belite_body(const Params& p, int tb, int b, char* smem) {
-  const int M = p.M, M1 = M + 1, n = p.n, tid = threadIdx.x;
-  const EliteLds C = elite_lds(M1);
+  const int M = p.M, M1 = M + 1, n = p.n, tid = tidx();
+  const EliteLds C = elite_lds(M1, blockDim.x >> 6);
   double* Gb = reinterpret_cast<double*>(smem + C.Gb);
   int* elite = reinterpret_cast<int*>(smem + C.misc);    // [11]
   int* info = elite + 16;                                 // [0] imin, [1] any NaN
@@ -2310,10 +2355,12 @@ DEVI void belite_body(const Params& p, int tb, int b, char* smem) {
   }
 }
 
+#ifndef MPCMMD_FUSED_TU
 __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   belite_body(p, tb, p.b0 + blockIdx.x, smem);
 }
+#endif
 
 // k_bgen: level 2 of the generators, one quad (4 lanes) per (candidate,
 // block of 16 positions).  The block prefix Phi_b (k_belite) is inverted
@@ -2332,10 +2379,10 @@ __global__ __launch_bounds__(kThreads) void k_belite(Params p, int tb) {
 HDI int sym11i(int a, int c) { return a <= c ? sym11(a, c) : sym11(c, a); }
 
 // the generators of 16-position block blk of candidate b on the calling quad
-// (lane q = threadIdx.x & 3); live = false: compute, store nothing
+// (lane q = tidx() & 3); live = false: compute, store nothing
 DEVI void bgen_quad(const Params& p, int b, int blk, bool live) {
   const int M = p.M, M1 = M + 1, nblk = (M1 + 15) / 16;
-  const int q = threadIdx.x & 3;
+  const int q = tidx() & 3;
   double* gen = p.gen + size_t(b) * pos_pad(M) * kGenStride;
   const double* Gb = p.phib + (size_t(b) * nblk + blk) * 66;
   // own rows a = q + 4 i; row 11 (q = 3, i = 2) is padding: an identity row
@@ -2410,13 +2457,15 @@ DEVI void bgen_quad(const Params& p, int b, int blk, bool live) {
   }
 }
 
+#ifndef MPCMMD_FUSED_TU
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_bgen(Params p) {
   const int nblk = (p.M + 1 + 15) / 16;
-  const int gq = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  const int gq = (blockIdx.x * blockDim.x + tidx()) >> 2;
   const bool live = gq < p.nb * nblk;  // quads stay whole: dead ones compute on a clamped block, store nothing
   const int gqc = live ? gq : p.nb * nblk - 1;
   bgen_quad(p, p.b0 + gqc / nblk, gqc % nblk, live);
 }
+#endif
 
 // The generators of block blk of candidate b on one wave (Params::gen_wave:
 // small batches, where k_bgen's chain of 11 pivots + 16 positions x (an
@@ -2462,7 +2511,7 @@ DEVI double rsq_nr(double d) {
 template <int NB>
 DEVI void bgen_wave(const Params& p, int b, int blk0, int bstride, double* xl) {
   const int M = p.M, M1 = M + 1, nblk = (M1 + 15) / 16, Pp = pos_pad(M);
-  const int lane = threadIdx.x & 63, r = lane & 15, h = lane >> 4;
+  const int lane = tidx() & 63, r = lane & 15, h = lane >> 4;
   double* gen = p.gen + size_t(b) * Pp * kGenStride;
   double* gm = p.genm + size_t(b) * Pp;
   int j0[NB];
@@ -2579,21 +2628,25 @@ DEVI void bgen_wave(const Params& p, int b, int blk0, int bstride, double* xl) {
 }
 
 constexpr int kGenWaveWaves = 4;
+#ifndef MPCMMD_FUSED_TU
 __global__ __launch_bounds__(64 * kGenWaveWaves) void k_bgen_wave(Params p) {
   __shared__ double xl[kGenWaveWaves][32];
   const int nblk = (p.M + 1 + 15) / 16;
-  const int w = threadIdx.x >> 6, gw = blockIdx.x * kGenWaveWaves + w;
+  const int w = tidx() >> 6, gw = blockIdx.x * kGenWaveWaves + w;
   if (gw >= p.nb * nblk) return;  // whole waves; no workgroup barrier below
   bgen_wave<1>(p, p.b0 + gw / nblk, gw % nblk, 0, xl[w]);
 }
+#endif
 
 // k_bsigma (last beta-iteration only): sigma_best when argmin is a new
 // sample -- its sigma coordinate drawn with the NEW generators (Q4,
 // compute_beta.py:133-145): y_M = mean_M + L_MM z_M + u_M . sum_{j<M} w_j z_j
 // the body of k_bsigma for candidate b when its argmin is a new sample;
-// red: (blockDim / 64) * 11 doubles of LDS
+// red: (kThreads / 64) * 11 doubles of LDS.  The sums are split over
+// kThreads threads whatever the workgroup size (the threads beyond add
+// nothing), so every caller forms the same bits.
 DEVI void bsigma_body(const Params& p, int tb, int b, double* red) {
-  const int M = p.M, tid = threadIdx.x;
+  const int M = p.M, tid = tidx();
   const int imin = p.bimin[b];
   const double* gen = p.gen + size_t(b) * pos_pad(M) * kGenStride;
   {
@@ -2602,7 +2655,7 @@ DEVI void bsigma_body(const Params& p, int tb, int b, double* red) {
     double part[11];
 #pragma unroll
     for (int a = 0; a < 11; ++a) part[a] = 0.0;
-    for (int j = tid; j < M; j += blockDim.x) {
+    for (int j = tid; j < M && tid < kThreads; j += kThreads) {
       const double zj = double(z[bz_index(j, si)]);
 #pragma unroll
       for (int a = 0; a < 11; ++a) part[a] += gen[size_t(j) * kGenRow + kGenW + a] * zj;
@@ -2612,7 +2665,7 @@ DEVI void bsigma_body(const Params& p, int tb, int b, double* red) {
       part[a] = wave_sum(part[a]);
     }
     __syncthreads();
-    if ((tid & 63) == 0)
+    if ((tid & 63) == 0 && tid < kThreads)
 #pragma unroll
       for (int a = 0; a < 11; ++a) red[(tid >> 6) * 11 + a] = part[a];
     __syncthreads();
@@ -2622,7 +2675,7 @@ DEVI void bsigma_body(const Params& p, int tb, int b, double* red) {
       double d = 0.0;
       for (int a = 0; a < 11; ++a) {
         double sa = 0.0;
-        for (int w2 = 0; w2 < (int)(blockDim.x >> 6); ++w2) sa += red[w2 * 11 + a];
+        for (int w2 = 0; w2 < kThreads / 64; ++w2) sa += red[w2 * 11 + a];
         d += gu[a] * sa;
       }
       const double zM = z[bz_index(M, si)];
@@ -2632,20 +2685,23 @@ DEVI void bsigma_body(const Params& p, int tb, int b, double* red) {
   }
 }
 
+#ifndef MPCMMD_FUSED_TU
 __global__ __launch_bounds__(kThreads) void k_bsigma(Params p, int tb) {
   __shared__ double red[(kThreads / 64) * 11];
   const int b = p.b0 + blockIdx.x;
   if (p.bimin[b] < kBetaElite) return;  // k_belite wrote it
   bsigma_body(p, tb, b, red);
 }
+#endif
 
 // ------------------------------------------------------------------------
 // k_mmdfinal: x_red / y_red of the best reduced set (compute_beta.py:465),
 // compute_mmd_obs (costs.py:173-186) and compute_mmd_lane (costs.py:121-135).
+#ifndef MPCMMD_FUSED_TU
 __global__ __launch_bounds__(64) void k_mmdfinal(Params p, int t) {
   __shared__ float cb[kMaxReduced], lb[kMaxReduced], ub[kMaxReduced], bt[kMaxReduced];
   __shared__ ReduceScratch rs;
-  const int b = blockIdx.x, n = p.n, H = p.H, O = p.O, lane = threadIdx.x;
+  const int b = blockIdx.x, n = p.n, H = p.H, O = p.O, lane = tidx();
   const Cfg cf = cfg_of(p, b / p.B);
   const float* ctrl = p.ctrl_n + size_t(b) * 2 * n * H;
   if (lane < n) {
@@ -2683,6 +2739,7 @@ __global__ __launch_bounds__(64) void k_mmdfinal(Params p, int t) {
     p.lane_cost[b] = ml + mu;
   }
 }
+#endif
 
 
 // ------------------------------------------------------------------------
@@ -2699,17 +2756,15 @@ __global__ __launch_bounds__(64) void k_mmdfinal(Params p, int t) {
 // selection by bselect_wave, kernel sums / K_red by bkernel_body, direct row
 // sums by bdirect_body, the QPs by bqp_solve (a quad each), elites by
 // belite_body, generators by bgen_wave, sigma_best by bsigma_body.
-// 8 waves (512 threads): the QP and generator phases need up to 256 VGPRs.
-constexpr int kSmallWaves = 8;
-constexpr int kSmallThreads = 64 * kSmallWaves;
-static_assert(kSmallThreads == kThreads, "belite_body / bsigma_body assume kThreads threads");
+// W = 16 waves (1024 threads, <= 128 VGPRs) for n <= 16, else 8 (the QPs of
+// n > 16 need up to 256 VGPRs): small_waves.
 HDI size_t small_sel_bytes(int R) { return size_t(64 * R + 8) * 8 + 64 * 4 + 128 * 4; }  // one wave's select LDS
-HDI size_t small_lds(int M, int n, int R) {
-  size_t b = size_t(kSmallWaves) * small_sel_bytes(R);
-  const size_t k = ker_lds(M, n, ker_scratch(M, n, 1, kSmallWaves)).total;
-  const size_t d = dir_lds(M, n).total, e = elite_lds(M + 1).total;
+HDI size_t small_lds(int M, int n, int R, int W) {
+  size_t b = size_t(W) * small_sel_bytes(R);
+  const size_t k = ker_lds(M, n, ker_scratch(M, n, 1, W)).total;
+  const size_t d = dir_lds(M, n).total, e = elite_lds(M + 1, W).total;
   const size_t q = size_t(kBetaSamples) * tri_stride(n) * 4;  // the QPs' K_red
-  const size_t g = size_t(kSmallWaves) * 4 * 32 * 8;             // bgen_wave<4>'s pivot columns
+  const size_t g = size_t(W) * 4 * 32 * 8;                        // bgen_wave<4>'s pivot columns
   const size_t gl = gen_lds_bytes(M);                             // the sampler's generator copy
   b = b > q ? b : q;
   b = b > g ? b : g;
@@ -2733,21 +2788,25 @@ DEVI int opaque_s(int v) {
 // apart from the kernel-sum body's own stamps): tools/stamp_small.py
 #define SMALL_STAMP(p, slot)                                                             \
   do {                                                                                   \
-    if (threadIdx.x == 0 && (p).dbgw)                                                    \
+    if (tidx() == 0 && (p).dbgw)                                                    \
       (p).dbgw[size_t(32768 + blockIdx.x) * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
-template <int NQ, int R, int G, int NP, int NV4, int GNB>
-__global__ __launch_bounds__(kSmallThreads) void k_bcem_small(Params p0) {
+#ifdef MPCMMD_FUSED_TU
+template <int NQ, int R, int G, int NP, int NV4, int GNB, int W>
+__global__ __launch_bounds__(64 * W) void k_bcem_small(Params p0) {
+  constexpr int kSmallWaves = W, kSmallThreads = 64 * W;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int cand = blockIdx.x;
-  const int tid = threadIdx.x;
+  const int tid = tidx();
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   for (int tb = 0; tb < kBetaIters; ++tb) {
-    Params p = p0;
-    p.n = opaque_s(p0.n);
-    p.M = opaque_s(p0.M);
-    p.b0 = opaque_s(p0.b0);
+    // the launch's Params read through a pointer laundered per iteration: no
+    // field (nor anything computed from one) is hoisted out of the loop
+    typedef const Params __attribute__((address_space(4)))* KParams;
+    KParams pk = (KParams)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(pk));
+    const Params& p = *(const Params*)pk;
     const int b = p.b0 + cand, M = p.M, n = p.n;
     const int ntri = tri_stride(n);
     // samples of this iteration (compute_beta.py:51-68); the first ones are
@@ -2824,9 +2883,11 @@ __global__ __launch_bounds__(kSmallThreads) void k_bcem_small(Params p0) {
     }
   }
 }
+#endif
 
 }  // namespace
 
+#ifndef MPCMMD_FUSED_TU
 bool mmdopt_supported(int n, int H, int O, std::string* why) {
   const int M = n * n;
   if (n > kMaxReduced) {
@@ -2949,6 +3010,8 @@ void launch_bqp(const Params& p, int tb, hipStream_t s) {
   switch (qp_np(p.n)) {
     case 8:
       return launch_bqp_quad<8>(p, tb, qps, s);
+    case 12:
+      return launch_bqp_quad<12>(p, tb, qps, s);
     case 16:
       return launch_bqp_quad<16>(p, tb, qps, s);
     case 24:
@@ -3015,27 +3078,42 @@ void launch_bgen(const Params& p, int tb, hipStream_t s) {
 }
 
 // (k_bcem_small's generators are bgen_wave's: handles with gen_wave only)
-bool bcem_small_ok(const Params& p) {
-  return p.gen_wave && p.n <= 24 && p.nb <= 512 && small_lds(p.M, p.n, 1) <= kLdsBudget;
-}
-
-void launch_bcem_small(const Params& p, hipStream_t s) {
-  const int n = p.n, M = p.M;
-  const dim3 grid(p.nb), block(kSmallThreads);
-  if (M <= 64)
-    hipLaunchKernelGGL((k_bcem_small<1, 1, 32, 8, 1, 1>), grid, block, small_lds(M, n, 1), s, p);
-  else if (M <= 128)
-    hipLaunchKernelGGL((k_bcem_small<2, 1, 32, 16, 1, 1>), grid, block, small_lds(M, n, 1), s, p);
-  else if (M <= 256)
-    hipLaunchKernelGGL((k_bcem_small<4, 1, 32, 16, 1, 2>), grid, block, small_lds(M, n, 1), s, p);
-  else if (M <= 512)
-    hipLaunchKernelGGL((k_bcem_small<8, 1, 32, 24, 2, 2>), grid, block, small_lds(M, n, 1), s, p);
-  else
-    hipLaunchKernelGGL((k_bcem_small<12, 1, 32, 24, 3, 2>), grid, block, small_lds(M, n, 1), s, p);
-}
-
 void launch_mmdfinal(const Params& p, int t, hipStream_t s) {
   hipLaunchKernelGGL(k_mmdfinal, dim3(p.Bt), dim3(64), 0, s, p, t);
 }
+
+#else
+// waves per workgroup: 16 while every phase fits 128 VGPRs (the QPs of n <=
+// 16, NP <= 16), else 8 (256 VGPRs)
+#ifndef MPCMMD_SMALL_W512
+#define MPCMMD_SMALL_W512 8  // waves at 256 < M <= 512 (experiment builds: -DMPCMMD_SMALL_W512=16)
+#endif
+HDI int small_waves(int M) { return M <= 256 ? 16 : (M <= 512 ? MPCMMD_SMALL_W512 : 8); }
+
+// M <= 256 (n <= 16): at n = 22 the per-iteration kernels, which spread each
+// phase over the whole chip, measured faster (CARLA n = 22: 63.0 vs 70.9 ms
+// per tick); the M > 256 instantiations stay for MPCMMD_FUSED experiments
+bool bcem_small_ok(const Params& p) {
+  return p.gen_wave && p.M <= 256 && p.nb <= 512 && small_lds(p.M, p.n, 1, small_waves(p.M)) <= kLdsBudget;
+}
+
+void launch_bcem_small(const Params& p, hipStream_t s) {
+  const int n = p.n, M = p.M, W = small_waves(M);
+  const dim3 grid(p.nb), block(64 * W);
+  const size_t lds = small_lds(M, n, 1, W);
+  if (M <= 64)
+    hipLaunchKernelGGL((k_bcem_small<1, 1, 32, 8, 1, 1, 16>), grid, block, lds, s, p);
+  else if (M <= 128)
+    hipLaunchKernelGGL((k_bcem_small<2, 1, 32, 12, 1, 1, 16>), grid, block, lds, s, p);
+  else if (M <= 256)
+    hipLaunchKernelGGL((k_bcem_small<4, 1, 32, 16, 1, 1, 16>), grid, block, lds, s, p);
+  else if (M <= 512)
+    hipLaunchKernelGGL((k_bcem_small<8, 1, 32, 24, 2, 16 / MPCMMD_SMALL_W512, MPCMMD_SMALL_W512>), grid, block, lds, s,
+                       p);
+  else
+    hipLaunchKernelGGL((k_bcem_small<12, 1, 32, 24, 3, 2, 8>), grid, block, lds, s, p);
+}
+
+#endif
 
 }  // namespace mpcmmd

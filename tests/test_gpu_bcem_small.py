@@ -1,5 +1,5 @@
 """k_bcem_small -- the 20 beta-iterations of a candidate in one workgroup, the
-small-batch path (num_batch <= 512, num_reduced <= 24: the reference's
+small-batch path (num_batch <= 512, num_reduced <= 16: the reference's
 num_batch = 100, BASELINE configs[4]) -- against the per-iteration kernels it
 replaces (MPCMMD_FUSED=0): every phase is the same device code, so a solve
 must give the same bits: per outer iteration the beta-CEM outputs (beta,
@@ -37,7 +37,7 @@ def _run(native, monkeypatch, fused, cost, n, B, H, O, T, xo=None, yo=None, carl
     return out, res
 
 
-@pytest.mark.parametrize("n,B,H,O", [(6, 32, 10, 3), (10, 100, 30, 4), (22, 100, 30, 10)])
+@pytest.mark.parametrize("n,B,H,O", [(6, 32, 10, 3), (10, 100, 30, 4), (16, 100, 30, 10)])
 def test_fused_bits_static(native, monkeypatch, n, B, H, O):
     T = 3
     ref, rr = _run(native, monkeypatch, False, "mmd_opt", n, B, H, O, T)

@@ -36,6 +36,12 @@ def main():
     print(f"n={n}: {live.sum()} workgroups; beta-iteration 5 span mean {(d[:, 7] - d[:, 0]).mean() / 100:.2f} us")
     for i, nm in enumerate(NAMES):
         print(f"  {nm:7s} mean {dt[:, i].mean():7.2f} us  p90 {np.percentile(dt[:, i], 90):7.2f} us")
+    # bkernel_body's own stamps (rows = workgroups, the last beta-iteration)
+    k = prob.handle.read("dbgw", np.uint64).astype(np.int64).reshape(65536, 8)[:100, :5]
+    k = k[k[:, 0] > 0]
+    kd = np.diff(k, axis=1) / 100.0
+    print("  kred sub-phases (last beta-iteration): setup+union %.2f, records+series %.2f, table %.2f, "
+          "entries %.2f us" % tuple(kd.mean(axis=0)))
 
 
 if __name__ == "__main__":
