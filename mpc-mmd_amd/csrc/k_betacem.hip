@@ -723,7 +723,7 @@ static_assert(kBzCols >= kNew, "sample tiles");
 // not depend on the batch it is solved in.
 constexpr int kChunkWavesMax = 12;
 HDI int sample_chunk(int nblk) {
-  int cl = 8;
+  int cl = nblk <= 8 ? 4 : 8;  // two chunks at M = 100 (k_bcem_small walks them in parallel)
   while ((nblk + cl - 1) / cl > kChunkWavesMax) cl <<= 1;
   return cl;
 }
@@ -1074,60 +1074,102 @@ __global__ __launch_bounds__(64 * kChunkWavesMax) void k_bsample_chunks(Params p
 }
 #endif
 
-// One tile of 16 samples of candidate b, every block walked by the calling
-// wave: k_bsample's walker with one tile per wave, its chunk folds included
-// (the same operands and operations per block, so the same bits), the
-// candidate's generators read from an LDS copy (lg: W plane, U plane, genm,
-// as in global memory) and the normals kZAhead blocks ahead in registers, so
-// the per-block wait is the MFMA chain, not a global load.  k_bcem_small's
-// sampler (its workgroup just wrote the generators).
+// k_bcem_small's sampler, from an LDS copy of the candidate's generators (lg:
+// W plane, U plane, genm, as in global memory; its workgroup just wrote them).
+// Two passes:
+//   bsample_tblocks  every block's T = strict_lower(W U^T) + diag(L_jj) (the
+//                    X MFMAs of block_mfma), once per block into LDS (Tl)
+//                    instead of once per tile
+//   bsample_unit_lds one (tile of 16 samples, chunk of blocks) per wave: the
+//                    earlier chunks' W^T Z sums first (S_pre, folded chunk by
+//                    chunk as the walker folds), then the chunk's blocks --
+//                    so the chunks of a tile run on separate waves
+// Per block the operands and MFMAs of block_mfma in its order, so the samples
+// are the per-iteration kernels' bits.  The normals (global, shared by every
+// candidate) come kZAhead blocks ahead in registers.
 constexpr int kZAhead = 4;
 HDI size_t gen_lds_bytes(int M) { return size_t(pos_pad(M)) * (2 * kGenRow + 1) * 8 + 16 * 8; }  // + wA's overreach
-DEVI void bsample_tile_lds(const Params& p, int tb, int b, int tile, const double* lg) {
+HDI size_t tblk_lds_bytes(int M) { return size_t(pos_pad(M) >> 4) * 4 * 64 * 8; }
+
+DEVI void bsample_tblocks(const Params& p, const double* lg, double* Tl, int w, int W) {
+  const int M = p.M, Pp = pos_pad(M), nblk = Pp >> 4;
+  const int lane = tidx() & 63, r = lane & 15, h = lane >> 4;
+  for (int blk = w; blk < nblk; blk += W) {
+    const int p0 = blk * 16;
+    const double* g = lg + size_t(p0 + r) * kGenRow;
+    const double* gu = lg + gen_uplane(Pp) + size_t(p0 + r) * kGenRow;
+    double wX[3], uX[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      wX[i] = g[kGenW + 4 * i + h];
+      uX[i] = gu[4 * i + h];
+    }
+    const double L = lg[2 * gen_uplane(Pp) + p0 + r];
+    d4 X = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) X = mfma64(wX[i], uX[i], X);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = h + 4 * i;
+      Tl[(size_t(blk) * 4 + i) * 64 + lane] = k < r ? X[i] : (k == r ? L : 0.0);
+    }
+  }
+}
+
+DEVI void bsample_unit_lds(const Params& p, int tb, int b, int tile, int chunk, const double* lg, const double* Tl) {
   const int M = p.M, Pp = pos_pad(M), nblk = Pp >> 4, cl = sample_chunk(nblk);
+  const int c0 = chunk * cl, c1 = min(nblk, c0 + cl);
   const int lane = tidx() & 63, r = lane & 15, h = lane >> 4, s0 = tile * 16;
   const double* LW = lg;
   const double* LU = lg + gen_uplane(Pp);
-  const double* LL = lg + 2 * gen_uplane(Pp);
   const float* z = p.beta_z + size_t(tb - 1) * Pp * kBzCols;
   const int ys = ygen_stride(M);
   float* plane = p.ygen + size_t(b) * kBzCols * ys;
-  d4 S[1] = {d4{0.0, 0.0, 0.0, 0.0}}, Sp[1] = {d4{0.0, 0.0, 0.0, 0.0}}, Y[1];
-  Sp[0][2] = h == 3 ? 1.0 : 0.0;  // row 11 of S_pre: the mean's coefficient
+  d4 S = d4{0.0, 0.0, 0.0, 0.0}, Sp = d4{0.0, 0.0, 0.0, 0.0};
+  Sp[2] = h == 3 ? 1.0 : 0.0;  // row 11 of S_pre: the mean's coefficient
   auto zload = [&](float (&zz)[4], int c) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) zz[k] = z[bz_index(c * 16 + 4 * k + h, s0 + r)];
   };
-  auto gload = [&](SampleBlock<1>& q, int p0) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) q.wA[k] = LW[size_t(p0 + 4 * k + h) * kGenRow + kGenW + r];
-    const double* g = LW + size_t(p0 + r) * kGenRow;
-    const double* gu = LU + size_t(p0 + r) * kGenRow;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      q.wX[i] = g[kGenW + 4 * i + h];
-      q.uX[i] = gu[4 * i + h];
-    }
-    q.L = LL[p0 + r];
-  };
   float zr[kZAhead][4];
 #pragma unroll
-  for (int u = 0; u < kZAhead; ++u) zload(zr[u], min(u, nblk - 1));
-  SampleBlock<1> q[2];
-  gload(q[0], 0);
-  for (int c = 0; c < nblk; c += kZAhead) {
+  for (int u = 0; u < kZAhead; ++u) zload(zr[u], min(u, c1 - 1));
+  const d4 zero = d4{0.0, 0.0, 0.0, 0.0};
+  for (int c = 0; c < c1; c += kZAhead) {
 #pragma unroll
     for (int u = 0; u < kZAhead; ++u) {
       const int cb = c + u;
-      if (cb < nblk) {  // wave-uniform
-        SampleBlock<1>& cur = q[u & 1];
+      if (cb < c1) {  // wave-uniform
+        const int p0 = cb * 16;
+        double zd[4], wA[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) cur.z[0][k] = zr[u][k];
-        zload(zr[u], min(cb + kZAhead, nblk - 1));
-        gload(q[(u + 1) & 1], min(cb + 1, nblk - 1) * 16);
-        block_mfma(cur, S, Sp, Y, r, h);
-        if ((cb + 1) % cl == 0) fold_chunk(Sp[0], S[0]);  // the walker's fold after the chunk's last block
-        block_store<1>(Y, plane, cb * 16, M, ys, s0, r, h);
+        for (int k = 0; k < 4; ++k) {
+          zd[k] = double(zr[u][k]);
+          wA[k] = LW[size_t(p0 + 4 * k + h) * kGenRow + kGenW + r];
+        }
+        zload(zr[u], min(cb + kZAhead, c1 - 1));
+        if (cb >= c0) {  // the chunk's block: Y = U S + T Z (block_mfma)
+          double uX[3], T[4];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) uX[i] = LU[size_t(p0 + r) * kGenRow + 4 * i + h];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) T[i] = Tl[(size_t(cb) * 4 + i) * 64 + lane];
+          double St[3];
+#pragma unroll
+          for (int k = 0; k < 3; ++k) St[k] = Sp[k] + S[k];
+          d4 Y = zero;
+#pragma unroll
+          for (int k = 0; k < 3; ++k) Y = mfma64(St[k], uX[k], k == 0 ? zero : Y);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) S = mfma64(wA[k], zd[k], S);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) Y = mfma64(zd[k], T[k], Y);
+          block_store<1>(&Y, plane, p0, M, ys, s0, r, h);
+        } else {  // an earlier chunk's block: its W^T Z into S_loc only
+#pragma unroll
+          for (int k = 0; k < 4; ++k) S = mfma64(wA[k], zd[k], S);
+        }
+        if ((cb + 1) % cl == 0) fold_chunk(Sp, S);  // the walker's fold after a chunk's last block
       }
     }
   }
@@ -2752,8 +2794,8 @@ __global__ __launch_bounds__(64) void k_mmdfinal(Params p, int t) {
 // candidate's intermediates (samples, selections, K_red, generators) in
 // global memory that this workgroup alone touches -- L2-resident at this
 // size.  Every phase is the body of its multi-kernel counterpart (same
-// operations, so the same bits): samples by bsample_tile_lds (a wave per tile),
-// selection by bselect_wave, kernel sums / K_red by bkernel_body, direct row
+// operations, so the same bits): samples by bsample_unit_lds (a wave per tile
+// and chunk), selection by bselect_wave, kernel sums / K_red by bkernel_body, direct row
 // sums by bdirect_body, the QPs by bqp_solve (a quad each), elites by
 // belite_body, generators by bgen_wave, sigma_best by bsigma_body.
 // W = 16 waves (1024 threads, <= 128 VGPRs) for n <= 16, else 8 (the QPs of
@@ -2765,7 +2807,7 @@ HDI size_t small_lds(int M, int n, int R, int W) {
   const size_t d = dir_lds(M, n).total, e = elite_lds(M + 1, W).total;
   const size_t q = size_t(kBetaSamples) * tri_stride(n) * 4;  // the QPs' K_red
   const size_t g = size_t(W) * 4 * 32 * 8;                        // bgen_wave<4>'s pivot columns
-  const size_t gl = gen_lds_bytes(M);                             // the sampler's generator copy
+  const size_t gl = ((gen_lds_bytes(M) + 15) & ~size_t(15)) + tblk_lds_bytes(M);  // the sampler's copy + T blocks
   b = b > q ? b : q;
   b = b > g ? b : g;
   b = b > gl ? b : gl;
@@ -2823,7 +2865,14 @@ __global__ __launch_bounds__(64 * W) void k_bcem_small(Params p0) {
         if (tid < 8) dst[ng + nm + tid] = double2{0.0, 0.0};
       }
       __syncthreads();
-      if (w < kSampleTiles) bsample_tile_lds(p, tb, b, w, reinterpret_cast<const double*>(smem));
+      {
+        const double* lg = reinterpret_cast<const double*>(smem);
+        double* Tl = reinterpret_cast<double*>(smem + ((gen_lds_bytes(M) + 15) & ~size_t(15)));
+        bsample_tblocks(p, lg, Tl, w, kSmallWaves);
+        __syncthreads();
+        const int nblk = pos_pad(M) >> 4, units = kSampleTiles * ((nblk + sample_chunk(nblk) - 1) / sample_chunk(nblk));
+        for (int u = w; u < units; u += kSmallWaves) bsample_unit_lds(p, tb, b, u % kSampleTiles, u / kSampleTiles, lg, Tl);
+      }
       __syncthreads();
       if (tb == 5) SMALL_STAMP(p, 1);
       char* sw = smem + size_t(w) * small_sel_bytes(R);
