@@ -1542,9 +1542,10 @@ DEVI void bkernel_body(const Params& p, int tb, int cand, int part, int split, i
     }
     __syncthreads();
     MPCMMD_STAMPW(p, 3);
-    // the (sample, entry) items of this part's samples spread over every
-    // thread, kJ items per thread in flight together (a wave per sample left
-    // most lanes idle at small n: 45 entries at n = 10)
+#ifdef MPCMMD_FUSED_TU
+    // k_bcem_small: the (sample, entry) items spread over every thread, kJ
+    // items per thread in flight together (a wave per sample leaves most
+    // lanes idle at small n: 45 entries at n = 10)
     constexpr int kJ = 4;
     const int ns = (kBetaSamples - s_lo - part + split - 1) / split, nitems = ns * nent;
     for (int i0 = tid; i0 < nitems; i0 += NT * kJ) {
@@ -1573,6 +1574,37 @@ DEVI void bkernel_body(const Params& p, int tb, int cand, int part, int split, i
         if (i0 + NT * j < nitems)
           kbase[size_t(s[j]) * ntri + e[j]] = kred_perturb(__builtin_amdgcn_exp2f(dv[j] * csg[s[j]]), e[j]);
     }
+#else
+    // a wave per sample of this part, all its lookups in flight together
+    // (entries lane + 64 j, j < kJ covers n <= 23; larger n loop)
+    constexpr int kJ = 4;
+    for (int s = s_lo + part + split * w; s < kBetaSamples; s += split * kKerWaves) {
+      const short* su = sl + s * n;
+      const float cs = csg[s];
+      float* kr = kbase + size_t(s) * ntri;
+      for (int e0 = 0; e0 < nent; e0 += 64 * kJ) {
+        int t[kJ];
+#pragma unroll
+        for (int j = 0; j < kJ; ++j) t[j] = tri[min(e0 + lane + 64 * j, nent - 1)];
+        int u0[kJ], u1[kJ];
+#pragma unroll
+        for (int j = 0; j < kJ; ++j) {
+          u0[j] = su[t[j] & 0xFF];
+          u1[j] = su[t[j] >> 8];
+        }
+        float dv[kJ];
+#pragma unroll
+        for (int j = 0; j < kJ; ++j) {
+          const int hi = max(u0[j], u1[j]), lo = min(u0[j], u1[j]);
+          dv[j] = T[hi * (hi - 1) / 2 + lo];
+        }
+#pragma unroll
+        for (int j = 0; j < kJ; ++j)
+          if (e0 + lane + 64 * j < nent)
+            kr[e0 + lane + 64 * j] = kred_perturb(__builtin_amdgcn_exp2f(dv[j] * cs), e0 + lane + 64 * j);
+      }
+    }
+#endif
   } else {
     // per-sample: the union records are dead, sl holds union ranks (urow maps back)
     float4* Fw = reinterpret_cast<float4*>(smem + C.scratch) + size_t(w) * n * Q;
