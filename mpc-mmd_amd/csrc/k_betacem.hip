@@ -2834,7 +2834,7 @@ __global__ __launch_bounds__(64) void k_mmdfinal(Params p, int t) {
 // n > 16 need up to 256 VGPRs): small_waves.
 HDI size_t small_sel_bytes(int R) { return size_t(64 * R + 8) * 8 + 64 * 4 + 128 * 4; }  // one wave's select LDS
 HDI size_t small_lds(int M, int n, int R, int W) {
-  size_t b = size_t(W) * small_sel_bytes(R);
+  size_t b = size_t(W) * small_sel_bytes(R) + size_t(kNew) * ygen_stride(M) * 4;  // + the staged sample rows
   const size_t k = ker_lds(M, n, ker_scratch(M, n, 1, W)).total;
   const size_t d = dir_lds(M, n).total, e = elite_lds(M + 1, W).total;
   const size_t q = size_t(kBetaSamples) * tri_stride(n) * 4;  // the QPs' K_red
@@ -2907,11 +2907,38 @@ __global__ __launch_bounds__(64 * W) void k_bcem_small(Params p0) {
       }
       __syncthreads();
       if (tb == 5) SMALL_STAMP(p, 1);
+      // the new samples' rows into LDS (after the waves' select scratch), so
+      // each wave's top-n walk reads its keys at LDS latency: a wave's chain of
+      // samples otherwise waits on one L2 round trip per sample.  Then
+      // bselect_wave's walk (samples first_sample(tb) = 11 .. 99: the elites'
+      // selections were carried) on the staged rows
+      const int ys = ygen_stride(M);
+      const float* Yl = reinterpret_cast<const float*>(smem + size_t(kSmallWaves) * small_sel_bytes(R));
+      {
+        const float4* src = reinterpret_cast<const float4*>(p.ygen + size_t(b) * kBzCols * ys);
+        float4* dst = reinterpret_cast<float4*>(smem + size_t(kSmallWaves) * small_sel_bytes(R));
+        for (int i = tid; i < kNew * (ys >> 2); i += kSmallThreads) dst[i] = src[i];
+      }
+      __syncthreads();
       char* sw = smem + size_t(w) * small_sel_bytes(R);
       unsigned long long* cand_l = reinterpret_cast<unsigned long long*>(sw);
       uint32_t* lm = reinterpret_cast<uint32_t*>(sw + size_t(64 * R + 8) * 8);
       int* scr = reinterpret_cast<int*>(sw + size_t(64 * R + 8) * 8 + 64 * 4);
-      bselect_wave<NQ, R, G>(p, tb, b, w, kSmallWaves, cand_l, lm, scr);
+      {
+        int32_t* sel = p.bsel + size_t(b) * kBetaSamples * n;
+        float* sig = p.bsig + size_t(b) * kBetaSamples;
+        auto row = [&](int s) {
+          const float* r = Yl + size_t(s - kBetaElite) * ys;
+          return [=](int j) { return r[j]; };
+        };
+        const int s_lo = first_sample(tb), lane = tid & 63;
+        if (s_lo + w < kBetaSamples) {
+          select_walk<NQ, R, G>(row, [&](int s) { return sel + s * n; }, s_lo + w, kBetaSamples, kSmallWaves, M, n,
+                                cand_l, lm, scr);
+          for (int s2 = s_lo + w + lane * kSmallWaves; lane < 16 && s2 < kBetaSamples; s2 += 16 * kSmallWaves)
+            sig[s2] = row(s2)(M);  // tb >= 1: rows are clipped when written
+        }
+      }
     } else {
       for (int e = tid; e < kBetaSamples * n; e += kSmallThreads) p.bsel[size_t(b) * kBetaSamples * n + e] = p.sel0[e];
       for (int e = tid; e < kBetaSamples; e += kSmallThreads) p.bsig[size_t(b) * kBetaSamples + e] = p.sig0[e];
