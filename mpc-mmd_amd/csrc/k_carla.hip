@@ -109,9 +109,16 @@ size_t risk_carla_lds(int O, int H, int S) {
   f = (f + 15) & ~size_t(15);
   f += size_t(S) * 8;
   f = (f + 15) & ~size_t(15);
-  return f + sizeof(ReduceScratch);
+  f += sizeof(ReduceScratch);
+  f = (f + 15) & ~size_t(15);
+  return f + size_t(256) * 4 * 4;  // the (row, step chunk) partial maxima
 }
 
+// Workgroup per candidate (256 threads).  The per-row maxima over the H steps
+// (collision residual over the obstacles, lane bars) are split over (row,
+// chunk of steps) threads, then each row's chunks are combined -- max is
+// exact in any order, so the bars are those of a sequential scan; the
+// desired-lane sums stay one sequential fp64 sum per row.
 __global__ __launch_bounds__(256) void k_risk_carla(Params p, int t, int mode) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int O = p.O, H = p.H, S = p.S, b = blockIdx.x, tid = threadIdx.x;
@@ -128,32 +135,60 @@ __global__ __launch_bounds__(256) void k_risk_carla(Params p, int t, int mode) {
   off += size_t(S) * 8;
   off = (off + 15) & ~size_t(15);
   ReduceScratch& rs = *reinterpret_cast<ReduceScratch*>(smem + off);
+  off += sizeof(ReduceScratch);
+  off = (off + 15) & ~size_t(15);
+  float* pc = reinterpret_cast<float*>(smem + off);  // [256]: chunk maxima c, l, u and the NaN flag
+  float* pl = pc + 256;
+  float* pu = pl + 256;
+  int* pn = reinterpret_cast<int*>(pu + 256);
   for (int i = tid; i < O * H; i += blockDim.x) {
     xo[i] = cf.obs[i];  // Frenet obstacle tracks x_obs_traj[:, :H], y_obs_traj[:, :H]
     yo[i] = cf.obs[O * H + i];
   }
   __syncthreads();
-  double s1 = 0.0, s2 = 0.0;  // ||y - y_des_1||_F^2, ||y - y_des_2||_F^2 over rows x steps
-  for (int r = tid; r < S; r += blockDim.x) {
+  const int K = max(1, int(blockDim.x) / S), L = (H + K - 1) / K;  // chunks per row, steps per chunk
+  if (tid < S * K) {
+    const int r = tid / K, c = tid - r * K;
     const float* q = p.rxy + (size_t(b) * S + r) * 2 * H;
-    float c = 0.0f, l = 0.0f, u = 0.0f;
+    float cm = 0.0f, l = 0.0f, u = 0.0f;
     bool nan = false;
-    for (int h = 0; h < H; ++h) {
+    for (int h = c * L; h < min(H, (c + 1) * L); ++h) {
       const float s = q[h], d = q[H + h];
       for (int o = 0; o < O; ++o) {
         const float f = f_bar_ab(s, d, xo[o * H + h], yo[o * H + h], p.obs_a2, p.obs_b2);
         nan |= (f != f);
-        c = fmaxf(c, f);
+        cm = fmaxf(cm, f);
       }
       nan |= (d != d);
       l = fmaxf(l, -d + p.y_lb);
       u = fmaxf(u, d - p.y_ub);
-      const double e1 = double(d) - double(p.y_des1), e2 = double(d) - double(p.y_des2);
+    }
+    pc[tid] = cm;
+    pl[tid] = l;
+    pu[tid] = u;
+    pn[tid] = nan ? 1 : 0;
+  }
+  double s1 = 0.0, s2 = 0.0;  // ||y - y_des_1||_F^2, ||y - y_des_2||_F^2 over rows x steps
+  for (int r = tid; r < S; r += blockDim.x) {
+    const float* q = p.rxy + (size_t(b) * S + r) * 2 * H;
+    for (int h = 0; h < H; ++h) {
+      const double e1 = double(q[H + h]) - double(p.y_des1), e2 = double(q[H + h]) - double(p.y_des2);
       s1 += e1 * e1;
       s2 += e2 * e2;
     }
+  }
+  __syncthreads();
+  for (int r = tid; r < S; r += blockDim.x) {
+    float cm = 0.0f, l = 0.0f, u = 0.0f;
+    int nan = 0;
+    for (int c = 0; c < K; ++c) {
+      cm = fmaxf(cm, pc[r * K + c]);
+      l = fmaxf(l, pl[r * K + c]);
+      u = fmaxf(u, pu[r * K + c]);
+      nan |= pn[r * K + c];
+    }
     const float qnan = __int_as_float(0x7fc00000);
-    cbar[r] = nan ? qnan : c;
+    cbar[r] = nan ? qnan : cm;
     lb[r] = nan ? qnan : l;
     ub[r] = nan ? qnan : u;
   }
@@ -203,8 +238,7 @@ void launch_frenet(const Params& p, hipStream_t s) {
 }
 
 void launch_risk_carla(const Params& p, int t, int mode, hipStream_t s) {
-  const int threads = p.S >= 256 ? 256 : ((p.S + 63) / 64) * 64;
-  hipLaunchKernelGGL(k_risk_carla, dim3(p.Bt), dim3(threads), risk_carla_lds(p.O, p.H, p.S), s, p, t, mode);
+  hipLaunchKernelGGL(k_risk_carla, dim3(p.Bt), dim3(256), risk_carla_lds(p.O, p.H, p.S), s, p, t, mode);
 }
 
 }  // namespace mpcmmd
