@@ -1385,8 +1385,12 @@ static_assert(kMomR == 12 && kMom == 12, "record layout: P_0..P_11 in float4s 0.
 
 // The body of k_bkernel for part `part` of candidate `cand` (of `split`),
 // NW waves (k_bkernel: 16; the small-batch fused kernel k_bcem_small: 8)
+// mom_l / feat_l: LDS copies of the candidate's series records and feature
+// rows (k_bcem_small, which keeps them for its 20 beta-iterations), else null
+// (read from global memory)
 template <int NW>
-DEVI void bkernel_body(const Params& p, int tb, int cand, int part, int split, int scratch, char* smem) {
+DEVI void bkernel_body(const Params& p, int tb, int cand, int part, int split, int scratch, char* smem,
+                       const float4* mom_l = nullptr, const float4* feat_l = nullptr) {
   constexpr int kKerWaves = NW;
   constexpr int NT = 64 * kKerWaves, Q = kFeatStride / 4;
   const int b = p.b0 + cand, M = p.M, n = p.n;
@@ -1449,8 +1453,8 @@ DEVI void bkernel_body(const Params& p, int tb, int cand, int part, int split, i
   const int Uu = misc[0];
   {
     // the union's records: staged in LDS when they fit, else read in place
-    const float4* mom = reinterpret_cast<const float4*>(p.bmom + size_t(b) * M * kMomStride);
-    const bool staged = size_t(Uu) * kMomStride * 4 <= size_t(scratch);  // block-uniform
+    const float4* mom = mom_l ? mom_l : reinterpret_cast<const float4*>(p.bmom + size_t(b) * M * kMomStride);
+    const bool staged = !mom_l && size_t(Uu) * kMomStride * 4 <= size_t(scratch);  // block-uniform
     float4* lrec = reinterpret_cast<float4*>(smem + C.scratch);
     if (staged)
       for (int i = tid; i < Uu * 4; i += NT) lrec[i] = mom[size_t(urow[i >> 2]) * 4 + (i & 3)];
@@ -1486,7 +1490,7 @@ DEVI void bkernel_body(const Params& p, int tb, int cand, int part, int split, i
   }
   MPCMMD_STAMP(p, 17);
   MPCMMD_STAMPW(p, 2);
-  const float4* fg = reinterpret_cast<const float4*>(p.featr + size_t(b) * M * kFeatStride);
+  const float4* fg = feat_l ? feat_l : reinterpret_cast<const float4*>(p.featr + size_t(b) * M * kFeatStride);
   float* kbase = p.bkred + size_t(b) * kBetaSamples * ntri;
   if (ker_tab_bytes(Uu) <= size_t(scratch)) {  // block-uniform
     float* T = reinterpret_cast<float*>(smem + C.scratch);
@@ -2849,14 +2853,9 @@ HDI size_t small_lds(int M, int n, int R, int W) {
   return b;
 }
 
-// an SGPR value the compiler cannot see through: each beta-iteration works on
-// its own copy of the shapes, so no phase's index arithmetic (the QP's 84
-// triangle addresses, say) is hoisted out of the iteration loop and kept live
-// across every other phase (spills)
-DEVI int opaque_s(int v) {
-  asm volatile("" : "+s"(v));
-  return v;
-}
+// the persistent LDS copies (k_bcem_small's persist): after the phases' space
+HDI size_t small_persist_off(int M, int n, int R, int W) { return (small_lds(M, n, R, W) + 15) & ~size_t(15); }
+HDI size_t small_persist_bytes(int M) { return size_t(M) * (kMomStride + kFeatStride) * 4; }
 
 // phase stamps of beta-iteration 5 (MPCMMD_STAMPW; rows 32768 + workgroup,
 // apart from the kernel-sum body's own stamps): tools/stamp_small.py
@@ -2868,12 +2867,29 @@ DEVI int opaque_s(int v) {
 
 #ifdef MPCMMD_FUSED_TU
 template <int NQ, int R, int G, int NP, int NV4, int GNB, int W>
-__global__ __launch_bounds__(64 * W) void k_bcem_small(Params p0) {
+__global__ __launch_bounds__(64 * W) void k_bcem_small(Params p0, int persist) {
   constexpr int kSmallWaves = W, kSmallThreads = 64 * W;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int cand = blockIdx.x;
   const int tid = tidx();
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // persist: the candidate's series records and feature rows (fixed for the
+  // outer iteration) copied once into LDS past the phases' space, for the
+  // kernel-sum phase of every beta-iteration
+  const float4* mom_l = nullptr;
+  const float4* feat_l = nullptr;
+  if (persist) {
+    const int M = p0.M, b = p0.b0 + cand;
+    float4* pm = reinterpret_cast<float4*>(smem + small_persist_off(M, p0.n, R, W));
+    float4* pf = pm + M * (kMomStride / 4);
+    const float4* gm = reinterpret_cast<const float4*>(p0.bmom + size_t(b) * M * kMomStride);
+    const float4* gf = reinterpret_cast<const float4*>(p0.featr + size_t(b) * M * kFeatStride);
+    for (int i = tid; i < M * (kMomStride / 4); i += kSmallThreads) pm[i] = gm[i];
+    for (int i = tid; i < M * (kFeatStride / 4); i += kSmallThreads) pf[i] = gf[i];
+    mom_l = pm;
+    feat_l = pf;
+    __syncthreads();
+  }
   for (int tb = 0; tb < kBetaIters; ++tb) {
     // the launch's Params read through a pointer laundered per iteration: no
     // field (nor anything computed from one) is hoisted out of the loop
@@ -2946,7 +2962,7 @@ __global__ __launch_bounds__(64 * W) void k_bcem_small(Params p0) {
     __syncthreads();
     if (tb == 5) SMALL_STAMP(p, 2);
     // K_mixed row sums and K_red (compute_beta.py:120-127)
-    bkernel_body<kSmallWaves>(p, tb, cand, 0, 1, int(ker_scratch(M, n, tb, kSmallWaves)), smem);
+    bkernel_body<kSmallWaves>(p, tb, cand, 0, 1, int(ker_scratch(M, n, tb, kSmallWaves)), smem, mom_l, feat_l);
     __syncthreads();
     if (tb == 5) SMALL_STAMP(p, 3);
     if (tb > 0) {
@@ -3208,18 +3224,20 @@ bool bcem_small_ok(const Params& p) {
 void launch_bcem_small(const Params& p, hipStream_t s) {
   const int n = p.n, M = p.M, W = small_waves(M);
   const dim3 grid(p.nb), block(64 * W);
-  const size_t lds = small_lds(M, n, 1, W);
+  const size_t lp = small_persist_off(M, n, 1, W) + small_persist_bytes(M);
+  const int persist = lp <= kLdsBudget;  // the records and features stay in LDS when they fit
+  const size_t lds = persist ? lp : small_lds(M, n, 1, W);
   if (M <= 64)
-    hipLaunchKernelGGL((k_bcem_small<1, 1, 32, 8, 1, 1, 16>), grid, block, lds, s, p);
+    hipLaunchKernelGGL((k_bcem_small<1, 1, 32, 8, 1, 1, 16>), grid, block, lds, s, p, persist);
   else if (M <= 128)
-    hipLaunchKernelGGL((k_bcem_small<2, 1, 32, 12, 1, 1, 16>), grid, block, lds, s, p);
+    hipLaunchKernelGGL((k_bcem_small<2, 1, 32, 12, 1, 1, 16>), grid, block, lds, s, p, persist);
   else if (M <= 256)
-    hipLaunchKernelGGL((k_bcem_small<4, 1, 32, 16, 1, 1, 16>), grid, block, lds, s, p);
+    hipLaunchKernelGGL((k_bcem_small<4, 1, 32, 16, 1, 1, 16>), grid, block, lds, s, p, persist);
   else if (M <= 512)
     hipLaunchKernelGGL((k_bcem_small<8, 1, 32, 24, 2, 16 / MPCMMD_SMALL_W512, MPCMMD_SMALL_W512>), grid, block, lds, s,
-                       p);
+                       p, persist);
   else
-    hipLaunchKernelGGL((k_bcem_small<12, 1, 32, 24, 3, 2, 8>), grid, block, lds, s, p);
+    hipLaunchKernelGGL((k_bcem_small<12, 1, 32, 24, 3, 2, 8>), grid, block, lds, s, p, persist);
 }
 
 #endif
