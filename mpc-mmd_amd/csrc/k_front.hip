@@ -112,8 +112,15 @@ DEVI void unwrap2(float& a0, float& a1, int lane, bool v1) {
 // res_norm is rounding noise, so reproducible transcendentals are what makes
 // the projection-elite order reproducible (DESIGN.md Numerics).
 DEVI float cr_atan2(float y, float x) { return float(atan2(double(y), double(x))); }
-DEVI float cr_cos(float a) { return float(cos(double(a))); }
 DEVI float cr_sin(float a) { return float(sin(double(a))); }
+// cos and sin from one fp64 sincos (OCML: one argument reduction, the values
+// of cos and sin), each rounded once
+DEVI void cr_sincos(float a, float& s, float& c) {
+  double sd, cd;
+  sincos(double(a), &sd, &cd);
+  s = float(sd);
+  c = float(cd);
+}
 
 struct Polar {
   float ca, sa, d;
@@ -124,7 +131,8 @@ struct Polar {
 // alpha = atan2(ws a, wc b), d = (a wc cos + b ws sin) / (a^2 cos^2 + b^2 sin^2)
 DEVI Polar obs_polar(float wc, float ws, const Params& p) {
   const float al = cr_atan2(ws * p.obs_a, wc * p.obs_b);
-  const float ca = cr_cos(al), sa = cr_sin(al);
+  float ca, sa;
+  cr_sincos(al, sa, ca);
   const float c1 = p.obs_a2 * (ca * ca) + p.obs_b2 * (sa * sa);
   const float c2 = (p.obs_a * wc) * ca + (p.obs_b * ws) * sa;
   return Polar{ca, sa, c2 / c1};
@@ -145,7 +153,8 @@ DEVI unsigned long long shfl_up_u64(unsigned long long v, int d) {
 
 // alpha = atan2(wy, wx); d = clip((wx cos + wy sin) / (cos^2 + sin^2), lo, hi)
 DEVI Polar polar_of(float alpha, float wx, float wy, float lo, float hi) {
-  const float ca = cr_cos(alpha), sa = cr_sin(alpha);
+  float ca, sa;
+  cr_sincos(alpha, sa, ca);
   const float c1 = ca * ca + sa * sa;
   const float c2 = wx * ca + wy * sa;
   float d = c2 / c1;

@@ -3,7 +3,7 @@
 each beta-CEM kernel, after a few steps of a bench workload (GPU box):
     python tools/stamps.py [workload]
 Slots: 0-1 k_bsample; k_bkernel 16 start, 19 series pairs done, 17 setup
-done, 18 K_red done, 20 end."""
+done, 18 K_red done, 20 end; k_front 40-46."""
 import os
 import sys
 
@@ -33,6 +33,11 @@ def main():
     print(f"{name}: bsample {us(0, 1):.1f} us")
     print(f"bkernel: series {us(16, 19):.1f} us, scan/order {us(19, 17):.1f} us, K_red {us(17, 18):.1f} us, "
           f"direct {us(18, 20):.1f} us, total {us(16, 20):.1f} us")
+    # k_front (workgroup 0): 40 staged, 41 guess + atan2, 42 unwrap, 43 initial multipliers (+ det sums),
+    # 44 compute_x, 45 compute_alph_d + multipliers, 46 controls + stores
+    names = ["guess+atan2", "unwrap", "polar+adj", "compute_x", "alph_d+adj", "controls+stores"]
+    print("front: " + ", ".join(f"{nm} {us(40 + i, 41 + i):.2f}" for i, nm in enumerate(names)) +
+          f"; total {us(40, 46):.2f} us")
 
 
 if __name__ == "__main__":
