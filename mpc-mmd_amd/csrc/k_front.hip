@@ -22,6 +22,7 @@
 // GEMVs with inverses built on the host (host_constants.cpp).  Elementwise
 // work is fp32 in the reference's operation order (-ffp-contract=off).
 #include "common.hpp"
+#include "cost.hpp"
 #include "frenet.hpp"
 #include "kernels.hpp"
 
@@ -594,6 +595,11 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
     p.lam_y[size_t(b) * kNv + lane] = vly;
   }
   if (lane == 0) p.res_norm[b] = rn;
+  if (!p.select_prep) {  // compute_cost's norms for k_select (cost.hpp), from the values just stored
+    double nk[11];
+    cost_norms(p, p.v_des[b / p.B], lane, y, xd, yd, xdd, ydd, steer, kapv, nk);
+    store_norms(p, b, lane, nk);
+  }
   MPCMMD_STAMP(p, 46);
 }
 

@@ -14,9 +14,11 @@
 // (O obstacles, staged in LDS) and the lane bars into running maxima, so
 // the stage reads only the candidate's H controls and the shared noise rows
 // (L2-resident, [H][S] for coalescing) and writes two floats per candidate.
+#include <algorithm>
 #include <cstdlib>
 
 #include "block.hpp"
+#include "cost.hpp"
 #include "draws.hpp"
 #include "kernels.hpp"
 #include "rng.hpp"
@@ -86,7 +88,12 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int O = p.O, H = p.H, S = p.S;
   RiskLds L = carve(smem, O, H, S);
-  const int b = blockIdx.x;
+  const int prep = select_prep_groups(p, blockDim.x);
+  if (int(blockIdx.x) < prep) {  // k_select's residual sort / cost norms, beside the rollouts
+    select_prep(p, t, blockIdx.x, reinterpret_cast<unsigned long long*>(smem));
+    return;
+  }
+  const int b = blockIdx.x - prep;
   const Cfg cf = cfg_of(p, b / p.B);
   for (int i = threadIdx.x; i < O * H; i += blockDim.x) {
     L.xo[i] = cf.obs[i];
@@ -816,9 +823,12 @@ void launch_risk_fused(const Params& p, int t, hipStream_t s) {
 }
 
 void launch_risk_baseline(const Params& p, int t, hipStream_t s) {
-  const size_t lds = risk_lds_bytes(p.O, p.H, p.S);
   const int threads = p.S >= 512 ? 512 : ((p.S + 63) / 64) * 64;
-  hipLaunchKernelGGL(k_risk_baseline, dim3(p.Bt), dim3(threads), lds, s, p, t);
+  const int prep = select_prep_groups(p, threads);
+  size_t n2 = 1;
+  while (n2 < size_t(p.B)) n2 <<= 1;
+  const size_t lds = std::max(risk_lds_bytes(p.O, p.H, p.S), prep ? n2 * 8 : size_t(0));
+  hipLaunchKernelGGL(k_risk_baseline, dim3(p.Bt + prep), dim3(threads), lds, s, p, t);
 }
 
 }  // namespace mpcmmd

@@ -3,16 +3,18 @@
 //
 //   argsort(res_norm) (full permutation, ellite_num_projection = B, Q6)  cem.py:233-248
 //   argsort(obs cost) over the permuted batch, top 20                   cem.py:264-289
-//   compute_cost of the 20 elites                                       cem_helper.py:232-262
+//   compute_cost of the 20 elites (norms from k_front, cost.hpp)        cem_helper.py:232-262
 //   compute_ellite_samples (top 5)                                      cem_helper.py:264-271
 //   compute_shifted_samples (mean/cov EMA, 8x8 Cholesky, B-5 draws)     cem_helper.py:280-314
 //   per-iteration result = elite 0 of the obstacle sort (Q1)            cem.py:308-315
 //
 // Plus stage "noise": the internal Philox draws of one outer iteration.
 #include "block.hpp"
+#include "cost.hpp"
 #include "draws.hpp"
 #include "kernels.hpp"
 #include "rng.hpp"
+#include "sort.hpp"
 
 namespace mpcmmd {
 
@@ -28,15 +30,48 @@ DEVI void wave_sync_lds() {
 constexpr int kMaxSortN = 4096;
 constexpr int kN = 100;
 
+// The stable argsort of configuration cf's projection residuals
+// (cem.py:233-248) into perm (LDS) and cf.tr_proj[t]: the words
+// (sort key << 32 | index) are distinct and their unsigned order is the
+// stable order.  Up to blockDim.x candidates one word per thread
+// (merge_sort_reg: wave bitonic + pairwise merges), beyond that the LDS
+// bitonic network.
+DEVI void sort_residuals(const Params& p, const Cfg& cf, int g0, int B, int t, unsigned long long* keys, int* perm) {
+  int N = 1;
+  while (N < B) N <<= 1;
+  const int i = threadIdx.x;
+  if (N <= int(blockDim.x)) {
+    unsigned long long a = i < B ? ((unsigned long long)sort_key(p.res_norm[g0 + i]) << 32) | unsigned(i) : ~0ull;
+    int idx;
+    a = merge_sort_reg(a, idx, N, keys);
+    if (i < B) {
+      const int v = int(a & 0xFFFFFFFFu);
+      perm[idx] = v;
+      cf.tr_proj[size_t(t) * B + idx] = v;
+    }
+    return;
+  }
+  for (int j = i; j < N; j += blockDim.x)
+    keys[j] = j < B ? ((unsigned long long)sort_key(p.res_norm[g0 + j]) << 32) | unsigned(j) : ~0ull;
+  bitonic_sort(keys, N);
+  for (int j = i; j < B; j += blockDim.x) {
+    const int v = int(keys[j] & 0xFFFFFFFFu);
+    perm[j] = v;
+    cf.tr_proj[size_t(t) * B + j] = v;
+  }
+}
+
 // Workgroups G.. (when kind != 0) draw iteration ahead_t's noise / gamma
 // table items (draws.hpp) meanwhile.
 __global__ __launch_bounds__(1024) void k_select(Params p, int t, int ahead_t, int kind) {
   __shared__ __attribute__((aligned(16))) unsigned long long keys[kMaxSortN];
   __shared__ int perm[kMaxSortN];
+  __shared__ float ocost[1024];
   __shared__ int el[kEliteCost];
   __shared__ float cost20[kEliteCost];
   __shared__ int cem5[kElite];
   __shared__ float pe[kElite][8];
+  __shared__ float pe20[kEliteCost][8];
   __shared__ double L[8][8];
   __shared__ double cvs[8][8];
   __shared__ float mean32[8];
@@ -51,25 +86,27 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t, int ahead_t, i
   int N = 1;
   while (N < B) N <<= 1;
   const int tid = threadIdx.x;
+  const bool window = B <= int(blockDim.x) && B >= kEliteCost;
 
   MPCMMD_STAMP(p, 32);
   // ---- argsort(res_norm), stable ------------------------------------------
-  for (int i = tid; i < N; i += blockDim.x)
-    keys[i] = i < B ? ((unsigned long long)sort_key(p.res_norm[g0 + i]) << 32) | unsigned(i) : ~0ull;
-  if (N <= int(blockDim.x)) bitonic_sort_reg(keys, N);
-  else bitonic_sort(keys, N);
-  for (int i = tid; i < B; i += blockDim.x) {
-    perm[i] = int(keys[i] & 0xFFFFFFFFu);
-    cf.tr_proj[size_t(t) * B + i] = perm[i];
+  const float oc = window && tid < B ? p.obs_cost[g0 + tid] : 0.0f;  // in flight during the sort
+  if (p.select_prep) {  // sorted by the risk launch (cost.hpp: select_prep)
+    for (int i = tid; i < B; i += blockDim.x) perm[i] = cf.tr_proj[size_t(t) * B + i];
+  } else {
+    sort_residuals(p, cf, g0, B, t, keys, perm);
   }
+  if (window && tid < B) ocost[tid] = oc;
   __syncthreads();
   MPCMMD_STAMP(p, 33);
+  // the mean / covariance entries of the update, loaded during the selection
+  const float cov0 = tid < 64 ? cf.cov[tid] : 0.0f, mean0 = tid < 8 ? cf.mean[tid] : 0.0f;
   // ---- argsort(obs cost) over the permuted batch -------------------------
-  if (B <= int(blockDim.x) && B >= kEliteCost) {  // only the 20 smallest words are needed: a window selection
+  if (window) {  // only the 20 smallest words are needed: a window selection
     __shared__ int wcnt;
     __shared__ unsigned long long wt0;
     const unsigned long long wv =
-        tid < B ? ((unsigned long long)sort_key(p.obs_cost[g0 + perm[tid]]) << 32) | unsigned(tid) : ~0ull;
+        tid < B ? ((unsigned long long)sort_key(ocost[perm[tid]]) << 32) | unsigned(tid) : ~0ull;
     block_smallest(wv, B, kEliteCost, keys, keys + 1024, wcnt, wt0, [&](int r, unsigned long long k) {
       const int e = perm[int(k & 0xFFFFFFFFu)];
       el[r] = e;  // candidate index within the configuration
@@ -88,93 +125,19 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t, int ahead_t, i
     __syncthreads();
   }
   MPCMMD_STAMP(p, 34);
-  // ---- compute_cost of the 20 elites: one wave each ----------------------
-  const int lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
-  for (int j = w; j < kEliteCost; j += nw) {
-    const int e = g0 + el[j];
-    const size_t plane = size_t(p.Bt) * kN, row = size_t(e) * kN;
-    const int t0 = lane, t1 = lane + 64;
-    const bool v1 = t1 < kN;
-    const int t1c = v1 ? t1 : kN - 1;
-    auto ld = [&](int k, int tt) { return p.traj[size_t(k) * plane + row + tt]; };
-    float y[2] = {ld(1, t0), ld(1, t1c)}, xd[2] = {ld(2, t0), ld(2, t1c)}, yd[2] = {ld(3, t0), ld(3, t1c)};
-    float xdd[2] = {ld(4, t0), ld(4, t1c)}, ydd[2] = {ld(5, t0), ld(5, t1c)};
-    float st[2] = {p.steer[row + t0], p.steer[row + t1c]};
-    // neighbours for the diffs
-    const float st_d0 = __shfl_down(st[0], 1, kWave);
-    const float st_f1 = readlane_f(st[1], 0);
-    const float st_n1 = __shfl_down(st[1], 1, kWave);
-    const float st_n0 = lane < 63 ? st_d0 : st_f1;
-    const float sv[2] = {st_n0 - st[0], st_n1 - st[1]};  // valid for t < 99
-    const float sv_d0 = __shfl_down(sv[0], 1, kWave);
-    const float sv_f1 = readlane_f(sv[1], 0);
-    const float sv_n1 = __shfl_down(sv[1], 1, kWave);
-    const float sv_n0 = lane < 63 ? sv_d0 : sv_f1;
-    const float sa[2] = {sv_n0 - sv[0], sv_n1 - sv[1]};  // valid for t < 98
-    double n_des = 0, n_st = 0, n_sv = 0, n_sa = 0, n_v = 0, n_sp = 0, n_svp = 0, n_ydd = 0, n_xdd = 0;
-    double n_des2 = 0, n_cen = 0;  // CARLA: second desired lane, centripetal penalty
-    float kap[2] = {0.f, 0.f};
-    if (p.carla) {
-      kap[0] = p.kappa_i[row + t0];
-      kap[1] = p.kappa_i[row + t1c];
-    }
+  // ---- compute_cost of the 20 elites, from k_front's norms (Params::cnorm)
+  if (tid < kEliteCost) {
+    const int e = g0 + el[tid];
+    double nk[11];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int tt = q == 0 ? t0 : t1;
-      if (tt >= kN) continue;
-      const double dd = double(y[q] - (p.carla ? p.y_des1 : -1.75f));
-      n_des += dd * dd;
-      if (p.carla) {  // carla/optimizer/cem_helper.py:529-544
-        const double d2 = double(y[q] - p.y_des2);
-        n_des2 += d2 * d2;
-        const double c = double(fmaxf(0.0f, fabsf((xd[q] * xd[q]) * kap[q]) - p.a_centr));
-        n_cen += c * c;
-      }
-      n_st += double(st[q]) * double(st[q]);
-      const float v = sqrtf(xd[q] * xd[q] + yd[q] * yd[q]);
-      const double dv = double(v - cf.v_des);
-      n_v += dv * dv;
-      const double sp = double(fmaxf(0.0f, fabsf(st[q]) - 0.6f));
-      n_sp += sp * sp;
-      n_ydd += double(ydd[q]) * double(ydd[q]);
-      n_xdd += double(xdd[q]) * double(xdd[q]);
-      if (tt < kN - 1) {
-        n_sv += double(sv[q]) * double(sv[q]);
-        const double svp = double(fmaxf(0.0f, fabsf(sv[q]) - 0.05f));
-        n_svp += svp * svp;
-      }
-      if (tt < kN - 2) n_sa += double(sa[q]) * double(sa[q]);
-    }
-    {  // the eleven wave totals at once (lanes 4 k .. 4 k + 3 hold total k)
-      const double nv[11] = {n_des, n_st, n_sv, n_sa, n_v, n_sp, n_svp, n_ydd, n_xdd, n_des2, n_cen};
-      const double z = wave_totals16_d(nv);
-      n_des = sqrt(readlane_d(z, 0));
-      n_st = sqrt(readlane_d(z, 4));
-      n_sv = sqrt(readlane_d(z, 8));
-      n_sa = sqrt(readlane_d(z, 12));
-      n_v = sqrt(readlane_d(z, 16));
-      n_sp = sqrt(readlane_d(z, 20));
-      n_svp = sqrt(readlane_d(z, 24));
-      n_ydd = sqrt(readlane_d(z, 28));
-      n_xdd = sqrt(readlane_d(z, 32));
-      n_des2 = sqrt(readlane_d(z, 36));
-      n_cen = sqrt(readlane_d(z, 40));
-    }
-    if (lane == 0) {
-      const double cobs = double(p.w_obs * p.obs_cost[e]);
-      const double clane = double(p.w_lane * p.lane_cost[e]);
-      double tot;
-      if (p.carla) {  // carla/optimizer/cem_helper.py:546-554; risk terms weighted in fp32 (cem.py:373-375)
-        const double cdes = double(p.w_des * p.lane_des[e]);
-        tot = (double(p.res_norm[e]) + 0.1 * n_v + 0.1 * (n_st + n_sv + n_sa) + 0.1 * (n_sp + n_svp) +
-               0.02 * n_ydd + 0.02 * n_xdd + 0.01 * (n_des * n_des2) + 0.1 * n_cen) +
-              cobs + clane + cdes;
-      } else {
-        tot = double(p.res_norm[e]) + 0.1 * n_v + 0.1 * (n_st + n_sv + n_sa) + 0.1 * (n_sp + n_svp) +
-              0.02 * n_ydd + 0.02 * n_xdd + 0.0 * n_des + cobs + 0.0 * clane;
-      }
-      cost20[j] = float(tot);
-    }
+    for (int k = 0; k < 11; ++k) nk[k] = p.cnorm[size_t(e) * kCnormStride + k];
+    cost20[tid] = cost_total(p, e, nk);
+  }
+  const float* pop = p.pop + (size_t(t & 1) * p.Bt + g0) * 8;
+  float* pop_next = p.pop + (size_t((t + 1) & 1) * p.Bt + g0) * 8;
+  if (tid >= 64 && tid < 64 + kEliteCost * 8) {  // the 20 elites' rows: the top 5 are among them
+    const int q = (tid - 64) >> 3, c = tid & 7;
+    pe20[q][c] = pop[size_t(el[q]) * 8 + c];
   }
   __syncthreads();
   MPCMMD_STAMP(p, 35);
@@ -189,11 +152,9 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t, int ahead_t, i
     if (r < kElite) cem5[r] = tid;
   }
   __syncthreads();
-  const float* pop = p.pop + (size_t(t & 1) * p.Bt + g0) * 8;
-  float* pop_next = p.pop + (size_t((t + 1) & 1) * p.Bt + g0) * 8;
   if (tid < kElite * 8) {
     const int q = tid >> 3, c = tid & 7;
-    pe[q][c] = pop[size_t(el[cem5[q]]) * 8 + c];
+    pe[q][c] = pe20[cem5[q]][c];
   }
   __syncthreads();
   // ---- compute_shifted_samples (fp64): weights per thread, mean entry c on
@@ -213,14 +174,14 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t, int ahead_t, i
       const int c = tid;
       double s = 0.0;
       for (int q = 0; q < kElite; ++q) s += wgt[q] * double(pe[q][c]);
-      mean32[c] = float((1.0 - 0.6) * double(cf.mean[c]) + 0.6 * s / sw);
+      mean32[c] = float((1.0 - 0.6) * double(mean0) + 0.6 * s / sw);  // mean0 = cf.mean[c]
     }
     wave_sync_lds();
     const int a = tid >> 3, c = tid & 7;
     const double ma = double(mean32[a]), mc = double(mean32[c]);
     double s = 0.0;
     for (int q = 0; q < kElite; ++q) s += wgt[q] * (double(pe[q][a]) - ma) * (double(pe[q][c]) - mc);
-    const float v = float((1.0 - 0.6) * double(cf.cov[a * 8 + c]) + 0.6 * s / sw + (a == c ? 0.01 : 0.0));
+    const float v = float((1.0 - 0.6) * double(cov0) + 0.6 * s / sw + (a == c ? 0.01 : 0.0));  // cov0 = cf.cov[tid]
     cvs[a][c] = double(v);
     cf.cov[a * 8 + c] = v;
     if (tid < 8) cf.mean[tid] = mean32[tid];

@@ -16,6 +16,7 @@ constexpr int kBetaSamples = 100;      // compute_beta.py:14
 constexpr int kBetaIters = 20;         // compute_beta.py:15
 constexpr int kBetaElite = 11;         // compute_beta.py:26
 constexpr int kEliteCost = 20;         // cem.py:140
+constexpr int kCnormStride = 12;       // doubles per candidate of Params::cnorm (11 norms)
 constexpr int kElite = 5;              // cem.py:138
 constexpr int kResultStride = 11 + 11 + 2 + 1 + 20 + kMaxReduced;  // cx, cy, lane, obs, sigma, res_beta, beta
 // generators per candidate: two planes of pos_pad(M) rows x kGenRow doubles,
@@ -97,6 +98,7 @@ struct Params {
   double* gtab;            // [G][gamma_tab_size] Beta-noise attempt tables of the current iteration
   void* mttab;             // [H][Bt] gamma constants per (step, candidate) of the fused rollouts (k_mt_tab)
   float* rbar;             // [3][Bt][S] per-row maxima (collision, lane lb, ub) of the fused rollouts
+  int32_t select_prep;     // the risk launch also sorts the residuals and forms the cost norms (cost.hpp)
   int32_t beta_dump;       // fused rollouts also store their Beta draws in bplane (MPCMMD_BETA_DUMP, tests)
   int32_t risk_rows;       // 1 (default): the row-lane rollouts over Beta planes; 0: fused (MPCMMD_RISK_FUSED=1)
   int32_t gen_wave;        // 1: beta-CEM generators by k_bgen_wave (a wave per block: the latency-bound small
@@ -115,6 +117,7 @@ struct Params {
   float* cy;               // [B][11]
   float* traj;             // [6][B][100]: x, y, xd, yd, xdd, ydd
   float* res_norm;         // [B]
+  double* cnorm;           // [B][kCnormStride] compute_cost's eleven norms (k_front, cost.hpp)
   float* acc;              // [B][100]
   float* steer;            // [B][100]
   float* obs_cost;         // [B]

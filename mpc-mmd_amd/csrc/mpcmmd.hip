@@ -130,6 +130,10 @@ struct mpcmmd_handle {
   // gamma table drawn for another iteration (the table has one slot)
   bool ahead_on = true;
   int ahead_t = -1;
+  // k_select's residual sort and cost norms run in the risk launch where it
+  // is k_risk_baseline (Params::select_prep); MPCMMD_SELECT_PREP=0: in
+  // k_select / k_front
+  bool prep_on = true;
   // small batches: the 20 beta-iterations as one launch (k_bcem_small);
   // MPCMMD_FUSED=0 keeps the per-iteration kernels
   bool fused_small = true;
@@ -691,6 +695,7 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     p.cx = (float*)h->alloc("cx", BT * kNvar * 4);
     p.cy = (float*)h->alloc("cy", BT * kNvar * 4);
     p.traj = (float*)h->alloc("traj", size_t(6) * BT * kNum * 4);
+    p.cnorm = (double*)h->alloc("cnorm", BT * kCnormStride * 8);
     p.res_norm = (float*)h->alloc("res_norm", BT * 4);
     p.acc = (float*)h->alloc("acc", BT * kNum * 4);
     p.steer = (float*)h->alloc("steer", BT * kNum * 4);
@@ -717,6 +722,7 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     if (const char* g = std::getenv("MPCMMD_GRAPH")) h->graphs = std::atoi(g) != 0;
     if (const char* g = std::getenv("MPCMMD_AHEAD")) h->ahead_on = std::atoi(g) != 0;
     if (const char* g = std::getenv("MPCMMD_FUSED")) h->fused_small = std::atoi(g) != 0;
+    if (const char* g = std::getenv("MPCMMD_SELECT_PREP")) h->prep_on = std::atoi(g) != 0;
     // the generators' variant is a property of the handle (its capacity), not
     // of a launch's candidate group: a candidate's bits do not depend on how
     // the batch is split into groups or whether k_bcem_small runs it
@@ -884,6 +890,10 @@ int begin_impl(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t
     h->cost = cost_kind;
     h->G = G;
     p.cost = cost_kind;
+    // k_select's residual sort and cost norms in the risk launch (cost.hpp):
+    // the baseline rollouts on Beta / Gaussian planes (k_risk_baseline)
+    p.select_prep = h->prep_on && !h->carla && p.risk_rows &&
+                    (cost_kind == MPCMMD_COST_CVAR || cost_kind == MPCMMD_COST_SAA || cost_kind == MPCMMD_COST_MMD_RANDOM);
     p.G = G;
     p.Bt = G * B;
     p.b0 = 0;
