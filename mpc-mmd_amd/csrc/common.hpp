@@ -38,6 +38,12 @@ template <int CTRL, int ROWS = 0xF>
 DEVI int dpp_i(int v) {
   return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, false);
 }
+// the same for controls whose every lane has a source (quad_perm, row_ror):
+// no old value, so no register to initialise
+template <int CTRL>
+DEVI int dpp_full(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
+}
 template <int CTRL, int ROWS = 0xF>
 DEVI double dpp_d(double v) {
   const long long b = __double_as_longlong(v);

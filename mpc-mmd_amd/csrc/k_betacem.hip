@@ -1882,34 +1882,45 @@ __global__ __launch_bounds__(64 * kDirWaves) void k_bdirect(Params p, int tb, in
 DEVI float quad_bcast(float v, int l) {
   const int b = __float_as_int(v);
   switch (l & 3) {
-    case 0: return __int_as_float(dpp_i<0x00>(b));
-    case 1: return __int_as_float(dpp_i<0x55>(b));
-    case 2: return __int_as_float(dpp_i<0xAA>(b));
-    default: return __int_as_float(dpp_i<0xFF>(b));
+    case 0: return __int_as_float(dpp_full<0x00>(b));
+    case 1: return __int_as_float(dpp_full<0x55>(b));
+    case 2: return __int_as_float(dpp_full<0xAA>(b));
+    default: return __int_as_float(dpp_full<0xFF>(b));
   }
 }
 DEVI double quad_bcast(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  int lo = int(b), hi = int(b >> 32);
   switch (l & 3) {
-    case 0: return dpp_d<0x00>(v);
-    case 1: return dpp_d<0x55>(v);
-    case 2: return dpp_d<0xAA>(v);
-    default: return dpp_d<0xFF>(v);
+    case 0: lo = dpp_full<0x00>(lo), hi = dpp_full<0x00>(hi); break;
+    case 1: lo = dpp_full<0x55>(lo), hi = dpp_full<0x55>(hi); break;
+    case 2: lo = dpp_full<0xAA>(lo), hi = dpp_full<0xAA>(hi); break;
+    default: lo = dpp_full<0xFF>(lo), hi = dpp_full<0xFF>(hi); break;
   }
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
 }
 // sum over the quad, bit-identical in its 4 lanes
 DEVI float quad_sum(float v) {
-  v = v + __int_as_float(dpp_i<0xB1>(__float_as_int(v)));  // quad_perm(1,0,3,2)
-  return v + __int_as_float(dpp_i<0x4E>(__float_as_int(v)));  // quad_perm(2,3,0,1)
+  v = v + __int_as_float(dpp_full<0xB1>(__float_as_int(v)));  // quad_perm(1,0,3,2)
+  return v + __int_as_float(dpp_full<0x4E>(__float_as_int(v)));  // quad_perm(2,3,0,1)
 }
 DEVI double quad_sum(double v) {
-  v = v + dpp_d<0xB1>(v);
-  return v + dpp_d<0x4E>(v);
+  auto sw = [](double x, auto f) {
+    const long long b = __double_as_longlong(x);
+    return __longlong_as_double((static_cast<long long>(f(int(b >> 32))) << 32) | static_cast<unsigned>(f(int(b))));
+  };
+  v = v + sw(v, [](int x) { return dpp_full<0xB1>(x); });
+  return v + sw(v, [](int x) { return dpp_full<0x4E>(x); });
 }
 // 1 / sqrt(x): v_rsq_f32 and one Newton step
 DEVI float rsqrt_nr(float x) {
   const float y = __builtin_amdgcn_rsqf(x);
   return y * fmaf(-0.5f * x, y * y, 1.5f);
 }
+
+// zero floats after the staged triangles (bqp_solve's padding rows and
+// reads past a row end: at most NP - 1 <= 31 floats past a triangle)
+constexpr int kQpZeros = 64;
 
 // K_red of the workgroup's QPs is staged in LDS first (consecutive
 // threads copy consecutive entries of one QP's triangle: coalesced), so the
@@ -1918,49 +1929,69 @@ DEVI float rsqrt_nr(float x) {
 DEVI void bqp_stage(const Params& p, int tb, float* kl) {
   const int n = p.n;
   const int s_lo = first_sample(tb), per = kBetaSamples - s_lo;
-  const int ntri = tri_stride(n);
+  const int ntri = tri_stride(n), n4 = ntri >> 2;
+  const int nq = blockDim.x >> 2, q0 = blockIdx.x * nq, total = p.nb * per;
   {  // the workgroup's K_red rows as float4s, consecutive threads on consecutive
      // float4s, every thread's loads issued before its first LDS store (one
-     // memory latency, not one per four rows)
-    const int nq = blockDim.x >> 2, q0 = blockIdx.x * nq, total = p.nb * per, n4 = ntri >> 2;
+     // memory latency, not one per four rows).  QP g = q0 + j (clamped to the
+     // last) is sample s0 + j of candidate c0 while s0 + j < per, else sample
+     // s0 + j - per of candidate c0 + 1 (nq < per): its triangle is the
+     // (j + (j >= jw ? s_lo : 0))-th past the first one's.  Float4 (j, r) of
+     // the staging advances by (T / n4, T % n4) per round of T threads.
+    const int c0 = q0 / per, s0 = q0 - c0 * per, jw = per - s0, jmax = min(nq, total - q0) - 1;
+    const float4* src = reinterpret_cast<const float4*>(p.bkred + (size_t(p.b0 + c0) * kBetaSamples + s_lo + s0) * ntri);
     float4* kl4 = reinterpret_cast<float4*>(kl);
+    const int T = blockDim.x, dj = T / n4, dr = T - dj * n4;
+    int j = int(tidx()) / n4, r = int(tidx()) - j * n4;
     constexpr int kU = 16;  // float4s per thread and round: 32 QPs x 58 float4s fit one round at n = 22
-    for (int i0 = 0; i0 < nq * n4; i0 += kU * int(blockDim.x)) {
+    for (int i0 = 0; i0 < nq * n4; i0 += kU * T) {
       float4 v[kU];
+      int jj[kU], rr[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const int i = min(i0 + int(tidx()) + u * int(blockDim.x), nq * n4 - 1);
-        const int j = i / n4, g = min(q0 + j, total - 1);
-        const float4* src = reinterpret_cast<const float4*>(
-            p.bkred + (size_t(p.b0 + g / per) * kBetaSamples + s_lo + g % per) * ntri);
-        v[u] = src[i - j * n4];
+        jj[u] = j;
+        rr[u] = r;
+        const int jc = min(j, jmax);
+        v[u] = src[(jc + (jc >= jw ? s_lo : 0)) * n4 + r];
+        j += dj;
+        r += dr;
+        if (r >= n4) {
+          r -= n4;
+          ++j;
+        }
       }
 #pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int i = i0 + int(tidx()) + u * int(blockDim.x);
-        if (i < nq * n4) kl4[i] = v[u];
-      }
+      for (int u = 0; u < kU; ++u)
+        if (jj[u] < nq) kl4[jj[u] * n4 + rr[u]] = v[u];
     }
+    if (int(tidx()) < kQpZeros) kl[nq * ntri + tidx()] = 0.0f;  // the padding rows' zeros
     __syncthreads();
   }
 }
 
 // QP of sample s of candidate b on the calling quad (lane q = tidx() & 3),
-// its K_red strict lower triangle at kr (LDS staging or global); ok = false:
-// compute on the clamped inputs, store nothing
+// its K_red strict lower triangle at kr (LDS staging); zr: kQpZeros zero
+// floats (the padding rows' entries), placed right after the last staged
+// triangle, so every read past a row end -- masked, never used -- lands on
+// K_red entries or zeros; ok = false: compute on the clamped inputs, store
+// nothing
 template <int NP>
-DEVI void bqp_solve(const Params& p, int b, int s, bool ok, const float* kr) {
+DEVI void bqp_solve(const Params& p, int b, int s, bool ok, const float* kr, const float* zr) {
   constexpr int T4 = NP / 4;
   const int n = p.n, M = p.M, q = tidx() & 3;
   const float* br = p.brow + (size_t(b) * kBetaSamples + s) * n;
   const double inv_m = double(1.0f / float(M));
   const float cdiag = 1.0f + 0.05f;
-  // entry (i, k < i) of K_red (k_bkernel's strict lower triangle); always a
-  // valid address (clamped), the value masked by the caller
-  auto kidx = [&](int i, int k) {
-    const int ic = min(i, n - 1);
-    return ic > 0 ? ic * (ic - 1) / 2 + max(min(k, ic - 1), 0) : 0;
-  };
+  // row i = 4t+q of K_red (k_bkernel's strict lower triangle: entry (i, k < i)
+  // at i (i-1)/2 + k), read at constant offsets k <= 4t+3 past the row start
+  // (entries k >= i are the next row's or zeros, masked); padding rows i >= n
+  // read zeros
+  const float* rowp[T4];
+#pragma unroll
+  for (int t = 0; t < T4; ++t) {
+    const int i = 4 * t + q;
+    rowp[t] = i < n ? kr + i * (i - 1) / 2 : zr;
+  }
   // own rows: A[t][k] = C[4t+q][k], k <= 4t+3; loaded as K_red (every load
   // unconditional, so they are all in flight together), factored in place
   float A[T4][NP];
@@ -1969,7 +2000,7 @@ DEVI void bqp_solve(const Params& p, int b, int s, bool ok, const float* kr) {
   for (int t = 0; t < T4; ++t) {
 #pragma unroll
     for (int k = 0; k < NP; ++k)
-      if (k <= 4 * t + 3) A[t][k] = kr[kidx(4 * t + q, k)];
+      if (k <= 4 * t + 3) A[t][k] = rowp[t][k];
     const int i = 4 * t + q;
     const float g = float(double(br[min(i, n - 1)]) * inv_m);
     a1[t] = i < n ? g : 0.0f;
@@ -1983,7 +2014,7 @@ DEVI void bqp_solve(const Params& p, int b, int s, bool ok, const float* kr) {
 #pragma unroll
     for (int k = 0; k <= 4 * t + 3; ++k) {
       const int i = 4 * t + q;
-      float v = (k < i && i < n) ? A[t][k] : 0.0f;
+      float v = k < i ? A[t][k] : 0.0f;  // padding rows: zeros
       if (k == i) v = i < n ? cdiag : 1.0f;
       A[t][k] = v;
     }
@@ -2004,8 +2035,19 @@ DEVI void bqp_solve(const Params& p, int b, int s, bool ok, const float* kr) {
     for (int c = k + 1; c < NP; ++c) {
       const int tc = c >> 2;
       const float lck = quad_bcast(A[tc][k], c & 3);  // L_ck from the lane owning row c
+      // rows (t, t + 1), t even, as packed pairs (v_pk_fma_f32: two fmaf)
+      int t = tc;
+      if (t & 1) {
+        A[t][c] = fmaf(-A[t][k], lck, A[t][c]);
+        ++t;
+      }
 #pragma unroll
-      for (int t = tc; t < T4; ++t) A[t][c] = fmaf(-A[t][k], lck, A[t][c]);
+      for (; t + 1 < T4; t += 2) {
+        const f2 x = __builtin_elementwise_fma(f2{-A[t][k], -A[t + 1][k]}, f2{lck, lck}, f2{A[t][c], A[t + 1][c]});
+        A[t][c] = x.x;
+        A[t + 1][c] = x.y;
+      }
+      if (t < T4) A[t][c] = fmaf(-A[t][k], lck, A[t][c]);
     }
   }
   // forward: L y = (g, 1)
@@ -2057,24 +2099,26 @@ DEVI void bqp_solve(const Params& p, int b, int s, bool ok, const float* kr) {
   // cost = beta^T K beta - 2 g^T beta in fp64, K = K_red re-read (unit
   // diagonal): r_i = sum_{k<i} K_ik beta_k by columns k, column k + 1's
   // entries in flight while column k is summed (two columns live, not the
-  // whole triangle); row i contributes beta_i (beta_i + 2 r_i)
+  // whole triangle); row i contributes beta_i (beta_i + 2 r_i).  An entry
+  // outside the triangle is a zero (padding rows) or masked to zero (k >= i
+  // in the diagonal block), and fma(0, beta_k, r) = r: the masked sum's bits
   double r[T4];
   float kc[T4], kn[T4];
 #pragma unroll
   for (int t = 0; t < T4; ++t) {
     r[t] = 0.0;
-    kc[t] = kr[kidx(4 * t + q, 0)];
+    kc[t] = rowp[t][0];
   }
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
 #pragma unroll
-    for (int t = (k + 1) >> 2; t < T4; ++t) kn[t] = kr[kidx(4 * t + q, min(k + 1, NP - 1))];
+    for (int t = (k + 1) >> 2; t < T4; ++t) kn[t] = rowp[t][min(k + 1, NP - 1)];
     __builtin_amdgcn_sched_barrier(0);
     const double bk = double(quad_bcast(bf[k >> 2], k & 3));
 #pragma unroll
     for (int t = k >> 2; t < T4; ++t) {
-      const int i = 4 * t + q;
-      r[t] = (k < i && i < n) ? fma(double(kc[t]), bk, r[t]) : r[t];
+      const float kv = t == (k >> 2) && !(k < 4 * t + q) ? 0.0f : kc[t];
+      r[t] = fma(double(kv), bk, r[t]);
       kc[t] = kn[t];
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -2105,7 +2149,7 @@ DEVI void bqp_quad(const Params& p, int tb, float* kl) {
   const int gqc = ok ? gq : 0;
   const int b = p.b0 + gqc / per, s = s_lo + gqc % per;
   bqp_stage(p, tb, kl);
-  bqp_solve<NP>(p, b, s, ok, kl + (tidx() >> 2) * tri_stride(p.n));
+  bqp_solve<NP>(p, b, s, ok, kl + (tidx() >> 2) * tri_stride(p.n), kl + (blockDim.x >> 2) * tri_stride(p.n));
 }
 
 // padded QP size (a multiple of 4: rows 4 t + q on quad lane q).  The
@@ -2841,7 +2885,7 @@ HDI size_t small_lds(int M, int n, int R, int W) {
   size_t b = size_t(W) * small_sel_bytes(R) + size_t(kNew) * ygen_stride(M) * 4;  // + the staged sample rows
   const size_t k = ker_lds(M, n, ker_scratch(M, n, 1, W)).total;
   const size_t d = dir_lds(M, n).total, e = elite_lds(M + 1, W).total;
-  const size_t q = size_t(kBetaSamples) * tri_stride(n) * 4;  // the QPs' K_red
+  const size_t q = (size_t(kBetaSamples) * tri_stride(n) + kQpZeros) * 4;  // the QPs' K_red and zeros
   const size_t g = size_t(W) * 4 * 32 * 8;                        // bgen_wave<4>'s pivot columns
   const size_t gl = ((gen_lds_bytes(M) + 15) & ~size_t(15)) + tblk_lds_bytes(M);  // the sampler's copy + T blocks
   b = b > q ? b : q;
@@ -2980,12 +3024,14 @@ __global__ __launch_bounds__(64 * W) void k_bcem_small(Params p0, int persist) {
       const float4* src = reinterpret_cast<const float4*>(p.bkred + (size_t(b) * kBetaSamples + s_lo) * ntri);
       float4* kl4 = reinterpret_cast<float4*>(smem);
       for (int i = tid; i < per * (ntri >> 2); i += kSmallThreads) kl4[i] = src[i];
+      if (tid < kQpZeros) reinterpret_cast<float*>(smem)[per * ntri + tid] = 0.0f;
       __syncthreads();
       static_assert(kSmallThreads / 4 >= kBetaSamples, "one quad per QP");
       const int g = tid >> 2;
       const bool ok = g < per;
       const int gc = ok ? g : 0;
-      bqp_solve<NP>(p, b, s_lo + gc, ok, reinterpret_cast<const float*>(smem) + size_t(gc) * ntri);
+      bqp_solve<NP>(p, b, s_lo + gc, ok, reinterpret_cast<const float*>(smem) + size_t(gc) * ntri,
+                    reinterpret_cast<const float*>(smem) + size_t(per) * ntri);
     }
     __syncthreads();
     if (tb == 5) SMALL_STAMP(p, 5);
@@ -3124,7 +3170,7 @@ void launch_bselect(const Params& p, int tb, hipStream_t s) {
 template <int NP>
 void launch_bqp_quad(const Params& p, int tb, int qps, hipStream_t s) {
   constexpr int T = qp_threads(NP);
-  const size_t lds = size_t(T / 4) * tri_stride(p.n) * 4;
+  const size_t lds = (size_t(T / 4) * tri_stride(p.n) + kQpZeros) * 4;
   hipLaunchKernelGGL((k_bqp<NP>), dim3((qps * 4 + T - 1) / T), dim3(T), lds, s, p, tb);
 }
 
