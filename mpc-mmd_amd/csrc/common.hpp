@@ -34,21 +34,25 @@ constexpr int kWave = 64;
 // quad_perm(1,0,3,2) 0xB1, quad_perm(2,3,0,1) 0x4E, row_ror:4 0x124,
 // row_ror:8 0x128, row_bcast:15 0x142, row_bcast:31 0x143.  Rows disabled by
 // ROWS read 0.
+// With every row enabled a lane without a source reads 0 through
+// bound_ctrl, so no old value is needed (no register to initialise); with
+// rows disabled those keep the old value 0.
 template <int CTRL, int ROWS = 0xF>
 DEVI int dpp_i(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, false);
+  if constexpr (ROWS == 0xF)
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
+  else
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, false);
 }
-// the same for controls whose every lane has a source (quad_perm, row_ror):
-// no old value, so no register to initialise
 template <int CTRL>
 DEVI int dpp_full(int v) {
-  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
+  return dpp_i<CTRL>(v);
 }
 template <int CTRL, int ROWS = 0xF>
 DEVI double dpp_d(double v) {
   const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, int(b), CTRL, ROWS, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), CTRL, ROWS, 0xF, false);
+  const int lo = dpp_i<CTRL, ROWS>(int(b));
+  const int hi = dpp_i<CTRL, ROWS>(int(b >> 32));
   return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
 }
 DEVI float readlane_f(float v, int lane) {
