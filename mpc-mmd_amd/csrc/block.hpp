@@ -127,10 +127,12 @@ DEVI void block_smallest(unsigned long long w, int B, int K, unsigned long long*
   if ((tid & 7) == 0 && tid < 8 * G) gm[tid >> 3] = m;
   if (tid == 0) {
     cnt = 0;
-    t0 = ~0ull;  // fewer than K groups: every word is in the window
+    t0 = ~0ull;     // fewer than K groups: every word is in the window
+    gm[G] = ~0ull;  // pads the pair reads (never smaller); slot G is no group's
   }
-  __syncthreads();
-  if (tid == 0) gm[G] = ~0ull;  // pads the pair reads (never smaller)
+  // the list pre-filled with ~0 (never smaller): the pair reads past its
+  // count need no pad written after the compaction
+  for (int i = tid; i < 8 * K + 2; i += blockDim.x) list[i] = ~0ull;
   __syncthreads();
   if (G > K && tid < G) {
     const unsigned long long mg = gm[tid];  // group tid's minimum
@@ -148,8 +150,6 @@ DEVI void block_smallest(unsigned long long w, int B, int K, unsigned long long*
   if (tid < B && w <= T0) list[atomicAdd(&cnt, 1)] = w;
   __syncthreads();
   const int c = cnt;
-  if (tid == 0) list[c] = ~0ull;
-  __syncthreads();
   const ulonglong2* l2 = reinterpret_cast<const ulonglong2*>(list);
   for (int a = tid; a < c; a += blockDim.x) {
     const unsigned long long ka = list[a];

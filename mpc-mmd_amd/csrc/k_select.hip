@@ -188,24 +188,38 @@ __global__ __launch_bounds__(1024) void k_select(Params p, int t, int ahead_t, i
     wave_sync_lds();
   }
   if (tid < 64) {
-    // Cholesky (lower) of the fp32 covariance, in fp64: column j's pivot on
-    // lane j, then its entries below on lanes i > j in parallel (each entry's
-    // sum in the serial algorithm's order, so the same bits)
-    for (int j = 0; j < 8; ++j) {
-      if (tid == j) {
-        double d = cvs[j][j];
-        for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k];
-        L[j][j] = sqrt(d);
-      }
-      wave_sync_lds();
-      if (tid > j && tid < 8) {
-        double s = cvs[tid][j];
-        for (int k = 0; k < j; ++k) s -= L[tid][k] * L[j][k];
-        L[tid][j] = s / L[j][j];
-      }
-      if (tid < j) L[tid][j] = 0.0;
-      wave_sync_lds();
+    // Cholesky (lower) of the fp32 covariance, in fp64: lane i < 8 holds row
+    // i in registers; column j's pivot from lane j's row, broadcast by
+    // readlane with row j's earlier entries, then the entries below on lanes
+    // i > j (each entry's sum in the serial algorithm's order, so the same
+    // bits); no LDS round trips between the columns
+    const int i = tid & 7;
+    double c[8], Lr[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      c[k] = cvs[i][k];
+      Lr[k] = 0.0;
     }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      double Ljk[8];
+#pragma unroll
+      for (int k = 0; k < j; ++k) Ljk[k] = readlane_d(Lr[k], j);
+      double d = c[j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) d -= Lr[k] * Lr[k];
+      const double piv = readlane_d(sqrt(d), j);
+      if (i == j) Lr[j] = piv;
+      if (i > j) {
+        double sm = c[j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) sm -= Lr[k] * Ljk[k];
+        Lr[j] = sm / piv;
+      }
+    }
+    if (tid < 8)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) L[tid][k] = Lr[k];
   }
   if (tid == 0) {
     // idx_min = argmin(cost_batch_temp) (== 0 unless NaN; jnp.argmin: first NaN)
