@@ -187,11 +187,24 @@ DEVI void gemv2_rows(const double* cx0, const double* cy0, const double* Ax, con
 
 template <bool kDet>
 __global__ __launch_bounds__(256) void k_front(Params p, int t) {
-  __shared__ float sB[3 * kN * kNv];
+  __shared__ __attribute__((aligned(16))) float sB[3 * kN * kNv];
   // CARLA: arc_vec [P], kappa [P] of the candidate block's configuration;
   // det: then its obstacle tracks x_obs [O][100], y_obs [O][100]
   extern __shared__ float sPath[];
-  for (int i = threadIdx.x; i < 3 * kN * kNv; i += blockDim.x) sB[i] = p.basis[i];
+  MPCMMD_STAMPW(p, 0);
+  {  // the basis (3 x 100 x 11 floats) as float4s, every load of a thread in
+     // flight before its first LDS store (one memory latency, not thirteen)
+    static_assert((3 * kN * kNv) % 4 == 0, "float4 staging");
+    constexpr int kQ = 3 * kN * kNv / 4, kPer = (kQ + 255) / 256;
+    const float4* b4 = reinterpret_cast<const float4*>(p.basis);
+    float4* s4 = reinterpret_cast<float4*>(sB);
+    float4 v[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) v[j] = b4[min(int(threadIdx.x) + 256 * j, kQ - 1)];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j)
+      if (int(threadIdx.x) + 256 * j < kQ) s4[threadIdx.x + 256 * j] = v[j];
+  }
   if (p.carla) {
     // every candidate of a block belongs to one configuration when B % 4 == 0
     // (the host checks); the block's first candidate names it
@@ -208,6 +221,7 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
   }
   __syncthreads();
   MPCMMD_STAMP(p, 40);
+  MPCMMD_STAMPW(p, 1);
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= p.Bt) return;
@@ -601,6 +615,7 @@ __global__ __launch_bounds__(256) void k_front(Params p, int t) {
     store_norms(p, b, lane, nk);
   }
   MPCMMD_STAMP(p, 46);
+  MPCMMD_STAMPW(p, 2);
 }
 
 }  // namespace
