@@ -84,7 +84,7 @@ size_t risk_lds_bytes(int O, int H, int S) {
 
 namespace {
 
-__global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) void k_risk_baseline(Params p, int t) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int O = p.O, H = p.H, S = p.S;
   RiskLds L = carve(smem, O, H, S);
@@ -94,6 +94,7 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
     return;
   }
   const int b = blockIdx.x - prep;
+  MPCMMD_STAMPW(p, 0);
   const Cfg cf = cfg_of(p, b / p.B);
   for (int i = threadIdx.x; i < O * H; i += blockDim.x) {
     L.xo[i] = cf.obs[i];
@@ -125,6 +126,7 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
     }
   }
   const bool window = !__syncthreads_or(any_nan);
+  MPCMMD_STAMPW(p, 1);
   const float* bpl = p.noise == 1 ? p.bplane + size_t(b) * 2 * H * S : nullptr;
   const size_t HS = size_t(H) * S;
   for (int r = threadIdx.x; r < S; r += blockDim.x) {
@@ -189,6 +191,7 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
     L.ub[r] = nan ? qnan : ub;
   }
   __syncthreads();
+  MPCMMD_STAMPW(p, 2);
   ReduceScratch& rs = *L.rs;
   float obs = 0.0f, lane = 0.0f;
   if (p.cost == 2) {  // cvar
@@ -209,6 +212,7 @@ __global__ __launch_bounds__(512) void k_risk_baseline(Params p, int t) {
     p.obs_cost[b] = obs;
     p.lane_cost[b] = lane;
   }
+  MPCMMD_STAMPW(p, 3);
 }
 
 // Beta-noise attempt table of outer iteration t (rng.hpp): one thread per
