@@ -78,6 +78,29 @@ DEVI void bitonic_sort_reg(unsigned long long* k, int N) {
   __syncthreads();
 }
 
+// block_sum of a double and an int together (one pair of barriers for both;
+// each total in block_sum's order, so the same bits)
+DEVI void block_sum2(double& v, int& c, double* sd, int* si) {
+  v = wave_sum(v);
+  c = wave_sum(c);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    sd[w] = v;
+    si[w] = c;
+  }
+  __syncthreads();
+  double s = 0.0;
+  int k = 0;
+  for (int i = 0; i < nw; ++i) {
+    s += sd[i];
+    k += si[i];
+  }
+  __syncthreads();
+  v = s;
+  c = k;
+}
+
 struct ReduceScratch {
   double d[16];
   int i[16];
@@ -236,8 +259,7 @@ DEVI float block_cvar(const float* vals, int S, unsigned long long* list, Reduce
       ++cnt;
     }
   }
-  sum = block_sum(sum, rs.d);
-  cnt = block_sum(cnt, rs.i);
+  block_sum2(sum, cnt, rs.d, rs.i);
   return cnt > 0 ? float(sum / double(cnt)) : 0.0f;
 }
 
