@@ -100,7 +100,9 @@ def kernel_work(w, name, launches, stats):
                of two gammas: 5 fp64 ops each; the combine: 6 fp64 ops and 11
                fp32 slots, the four transcendentals at their double issue
                cost) against one lane-slot per lane and cycle (39.3 T/s)
-      risk_baseline  B x S rollouts x H steps x (bicycle 40 + 9 per obstacle (+ beta 320))"""
+      risk_baseline  B x S rollouts x H steps x (bicycle 40 + 9 per obstacle);
+               the Beta draws are k_beta_planes' work (its own model), the
+               rollouts read them"""
     B, H, O = w["num_batch"], w["num_prime"], w["num_obs"]
     n = w["num_reduced"]
     M = n * n
@@ -122,8 +124,7 @@ def kernel_work(w, name, launches, stats):
     if name == "beta_planes":
         return "valu-issue", "T lane-slots/s", launches * B * n * H * 2 * 27, VALU64_PEAK_TOPS
     if name == "risk_baseline":
-        beta = 2 * 160 if w["noise"] == "beta" else 0
-        return "valu", "T lane-ops/s", launches * B * n * H * (40 + O * 9 + beta), VALU_PEAK_TOPS
+        return "valu", "T lane-ops/s", launches * B * n * H * (40 + O * 9), VALU_PEAK_TOPS
     return None
 
 
@@ -181,36 +182,62 @@ def step_roofline(w, busy, profile_steps, stats, ms_per_step, workload):
     t = ms_per_step / 1e3
     counter = 0.0
     have = True
+    tags = set()
     for k, (launches, _) in busy.items():
-        v = pmc_traffic(workload, k)
+        v, tag = pmc_traffic(workload, k, with_tag=True)
         if v is None:
             have = False
             continue
+        tags.add(tag)
         counter += v * launches * per
     bound = {t_hbm: "hbm", t_valu: "valu", t_mfma: "mfma-fp64"}[t_lower]
     return {"t_lower_ms": t_lower * 1e3, "bound": bound, "achieved": t_lower / t, "t_hbm_ms": t_hbm * 1e3,
             "t_valu_ms": t_valu * 1e3, "t_mfma_ms": t_mfma * 1e3, "bytes_alg": alg,
             "alg_hbm_frac": alg / (t * HBM_PEAK_GBS * 1e9), "valu_lane_slots": slots, "mfma_flop": mflop,
-            "counter_bytes": counter if have else None,
+            "counter_bytes": counter if have else None, "counter_profiles": sorted(tags),
             "hbm_frac": counter / (t * HBM_PEAK_GBS * 1e9) if have else None,
             "mfma_peak_tflops": MFMA64_MEASURED_TFLOPS}
 
 
-def pmc_traffic(workload, kernel):
-    """HBM bytes per launch of `kernel` in `workload` from the committed PMC
-    passes (the newest of profiles/r0N_pmc_traffic.json; {workload: {kernel:
-    bytes}}: 2 x FETCH_SIZE + WRITE_SIZE per the MI355X guide's gfx950
-    correction), or None."""
-    for tag in ("r04f", "r04e", "r03d", "r03c", "r03b", "r03", "r02", "r01"):
-        path = os.path.join(ROOT, "profiles", f"{tag}_pmc_traffic.json")
+def _pmc_files():
+    """The committed PMC traffic files, newest first: profiles/rNN[x]_pmc_traffic.json
+    ({workload: {kernel: bytes}}) and rNN[x]_pmc_traffic_<workload>.json
+    ({kernel: bytes}; <workload> "mmdopt" = mmd_opt)."""
+    import re
+    pat = re.compile(r"^r(\d\d)([a-z]?)_pmc_traffic(?:_([a-z0-9]+))?\.json$")
+    out = []
+    try:
+        names = os.listdir(os.path.join(ROOT, "profiles"))
+    except OSError:
+        return out
+    for nm in names:
+        m = pat.match(nm)
+        if m:
+            wl = {"mmdopt": "mmd_opt"}.get(m.group(3), m.group(3))
+            out.append(((int(m.group(1)), m.group(2)), f"r{m.group(1)}{m.group(2)}", wl, nm))
+    out.sort(key=lambda x: x[0], reverse=True)
+    return out
+
+
+def pmc_traffic(workload, kernel, with_tag=False):
+    """HBM bytes per launch of `kernel` in `workload` from the newest committed
+    PMC pass that measured it (2 x FETCH_SIZE + WRITE_SIZE per the MI355X
+    guide's gfx950 correction), or None; with_tag: (bytes, profile tag)."""
+    for _, tag, wl, nm in _pmc_files():
+        if wl is not None and wl != workload:
+            continue
         try:
-            with open(path) as f:
-                v = json.load(f).get(workload, {}).get(kernel)
-            if v is not None:
-                return v
+            with open(os.path.join(ROOT, "profiles", nm)) as f:
+                d = json.load(f)
+            d = d if wl is not None else d.get(workload, {})
+            v = d.get(kernel)
+            if v is None:   # the library's kernel id names the family (beta_planes: k_beta_planes_c, ...)
+                v = next((d[k] for k in sorted(d) if k.startswith(kernel + "_")), None)
         except (OSError, ValueError, AttributeError):
             continue
-    return None
+        if v is not None:
+            return (v, tag) if with_tag else v
+    return (None, None) if with_tag else None
 
 
 def make_workload(w, rank):
@@ -345,7 +372,7 @@ def run_workload(name, steps, warmup, profile_steps, rank, world, local, dist=No
         scale = model[4] if len(model) > 4 else 1e12  # unit of `achieved` (T/s; GB/s for HBM bounds)
         roof.update(bound=bound, unit=unit, peak=peak, achieved=amount / launches / avg_s / scale)
         roof["frac"] = roof["achieved"] / peak
-    roof["traffic"] = pmc_traffic(name, dom)
+    roof["traffic"], roof["traffic_profile"] = pmc_traffic(name, dom, with_tag=True)
     roof["kernel"] = dom
     roof["avg_us"] = avg_s * 1e6
     if w["cost"] == "mmd_opt":  # k_bkernel work counters over the profiled pass
@@ -360,7 +387,7 @@ CARLA = os.path.join(PKG, "carla")
 # BASELINE configs[4]: the CARLA optimizer (carla/optimizer/cem.py), mmd_opt + cvar back to back per
 # simulator tick at H = 60, num_batch 100 (cem.py:138), num_obs 3 (README CARLA commands), replayed ticks
 CARLA_WORKLOAD = dict(desc="CARLA replay (synthetic Town05 recording), compute_cem_mmd + compute_cem_cvar back to "
-                           "back per tick, H=60, num_batch=100, num_obs=3, num_reduced_set=10 (mmd: 100 mother rows)",
+                           "back per tick, H=60, num_batch=100, num_obs=3, num_reduced_set={n} (mmd: {M} mother rows)",
                       baseline="configs[4]", num_reduced=10, num_obs=3, num_prime=60, noise="gaussian", level=0.1,
                       num_batch=100, town="Town05", budget_ms=50.0)
 
@@ -454,7 +481,8 @@ def run_carla(ticks, warmup, local, n=None):
         if i >= warmup:
             conc.append(time.perf_counter() - t0)
     conc = np.array(conc) * 1e3
-    return {"baseline": w["baseline"], "workload": w["desc"], "num_reduced_set": w["num_reduced"], "ticks": ticks,
+    desc = w["desc"].format(n=w["num_reduced"], M=w["num_reduced"] ** 2)
+    return {"baseline": w["baseline"], "workload": desc, "num_reduced_set": w["num_reduced"], "ticks": ticks,
             "value": 1e3 / float(np.mean(a[:, 3])), "unit": "ticks/s",
             "ms_per_tick": float(np.mean(a[:, 3])), "median_ms_per_tick": float(np.median(a[:, 3])),
             "p90_ms_per_tick": float(np.percentile(a[:, 3], 90)), "budget_ms": w["budget_ms"],

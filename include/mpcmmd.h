@@ -24,7 +24,8 @@
 extern "C" {
 #endif
 
-#define MPCMMD_ABI_VERSION 3
+/* 4: MPCMMD_COST_DET (CARLA compute_cem_det), mpcmmd_handle_info */
+#define MPCMMD_ABI_VERSION 4
 
 /* status codes */
 #define MPCMMD_OK 0
@@ -145,6 +146,28 @@ void mpcmmd_destroy(mpcmmd_handle* h);
  * mpcmmd_create(cfg, out) == mpcmmd_create_batch(cfg, 1, out). */
 int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_handle** out);
 int32_t mpcmmd_max_configs(mpcmmd_handle* h);
+
+/* Implementation choices of a handle, fixed at create (no reference
+ * counterpart: the reference has one JAX program).  name:
+ *   "gen_wave"     1: the beta-CEM generators by one wave per 16-position block
+ *                  (k_bgen_wave, fp64 MFMA), 0: a quad per block (k_bgen).  The
+ *                  two sum in different orders, so their bits differ (both
+ *                  within the parity tolerances).  Default: 1 when the handle's
+ *                  capacity max_configs * num_batch <= 512 and num_reduced <= 24
+ *                  -- the SAME problem can therefore give different bits on a
+ *                  handle of 512 and one of 1024 candidates, or with another
+ *                  max_configs.  Pin it with the environment variable
+ *                  MPCMMD_GENWAVE=0/1 (read at create) to compare batch sizes.
+ *   "select_prep"  1: for cvar / saa / mmd_random the risk launch (stage 2) also
+ *                  sorts the residuals and forms compute_cost's norms, so stage 3
+ *                  needs stage 2 of the same iteration (MPCMMD_SELECT_PREP=0: in
+ *                  stages 1 and 3; same bits either way)
+ *   "fused_small"  1: small batches run the 20 beta-iterations as one launch
+ *                  (k_bcem_small; same bits as the per-iteration kernels)
+ *   "groups"       beta-CEM candidate groups on their own streams (same bits)
+ *   "capacity"     max_configs * num_batch
+ * Writes *value; MPCMMD_E_INVALID for an unknown name. */
+int mpcmmd_handle_info(mpcmmd_handle* h, const char* name, int64_t* value);
 
 /* Run on a caller-owned hipStream_t instead of the handle's own stream. */
 int mpcmmd_set_stream(mpcmmd_handle* h, void* hip_stream);

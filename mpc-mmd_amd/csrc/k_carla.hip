@@ -111,7 +111,7 @@ size_t risk_carla_lds(int O, int H, int S) {
   f = (f + 15) & ~size_t(15);
   f += sizeof(ReduceScratch);
   f = (f + 15) & ~size_t(15);
-  return f + size_t(256) * 4 * 4;  // the (row, step chunk) partial maxima
+  return f + size_t(std::max(256, S)) * 4 * 4;  // the (row, step chunk) partial maxima
 }
 
 // Workgroup per candidate (256 threads).  The per-row maxima over the H steps
@@ -137,18 +137,20 @@ __global__ __launch_bounds__(256) void k_risk_carla(Params p, int t, int mode) {
   ReduceScratch& rs = *reinterpret_cast<ReduceScratch*>(smem + off);
   off += sizeof(ReduceScratch);
   off = (off + 15) & ~size_t(15);
-  float* pc = reinterpret_cast<float*>(smem + off);  // [256]: chunk maxima c, l, u and the NaN flag
-  float* pl = pc + 256;
-  float* pu = pl + 256;
-  int* pn = reinterpret_cast<int*>(pu + 256);
+  // [S K] (<= max(256, S)): chunk maxima c, l, u and the NaN flag
+  const int K = max(1, int(blockDim.x) / S), L = (H + K - 1) / K;  // chunks per row, steps per chunk
+  const int NP = max(256, S);
+  float* pc = reinterpret_cast<float*>(smem + off);
+  float* pl = pc + NP;
+  float* pu = pl + NP;
+  int* pn = reinterpret_cast<int*>(pu + NP);
   for (int i = tid; i < O * H; i += blockDim.x) {
     xo[i] = cf.obs[i];  // Frenet obstacle tracks x_obs_traj[:, :H], y_obs_traj[:, :H]
     yo[i] = cf.obs[O * H + i];
   }
   __syncthreads();
-  const int K = max(1, int(blockDim.x) / S), L = (H + K - 1) / K;  // chunks per row, steps per chunk
-  if (tid < S * K) {
-    const int r = tid / K, c = tid - r * K;
+  for (int e = tid; e < S * K; e += blockDim.x) {  // S > 256: K = 1, rows strided over the threads
+    const int r = e / K, c = e - r * K;
     const float* q = p.rxy + (size_t(b) * S + r) * 2 * H;
     float cm = 0.0f, l = 0.0f, u = 0.0f;
     bool nan = false;
@@ -163,10 +165,10 @@ __global__ __launch_bounds__(256) void k_risk_carla(Params p, int t, int mode) {
       l = fmaxf(l, -d + p.y_lb);
       u = fmaxf(u, d - p.y_ub);
     }
-    pc[tid] = cm;
-    pl[tid] = l;
-    pu[tid] = u;
-    pn[tid] = nan ? 1 : 0;
+    pc[e] = cm;
+    pl[e] = l;
+    pu[e] = u;
+    pn[e] = nan ? 1 : 0;
   }
   double s1 = 0.0, s2 = 0.0;  // ||y - y_des_1||_F^2, ||y - y_des_2||_F^2 over rows x steps
   for (int r = tid; r < S; r += blockDim.x) {

@@ -134,6 +134,10 @@ struct mpcmmd_handle {
   // is k_risk_baseline (Params::select_prep); MPCMMD_SELECT_PREP=0: in
   // k_select / k_front
   bool prep_on = true;
+  // the iteration whose residual sort and cost norms the risk launch made
+  // (-1: none since begin / the last front stage); stage 3 with select_prep
+  // needs them for its own t
+  int prep_t = -1;
   // small batches: the 20 beta-iterations as one launch (k_bcem_small);
   // MPCMMD_FUSED=0 keeps the per-iteration kernels
   bool fused_small = true;
@@ -411,6 +415,7 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
       break;
     case 1:
       h->launch(kKFront, [&] { launch_front(p, t, h->stream); });
+      h->prep_t = -1;  // new residuals; with select_prep no cost norms until stage 2
       break;
     case 2:
       if (p.cost == MPCMMD_COST_DET) break;  // compute_cem_det: no rollouts, zero risks (carla/optimizer/cem.py:717-722)
@@ -433,9 +438,14 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
       } else {
         if (p.noise == MPCMMD_NOISE_BETA) h->launch(kKBetaPlanes, [&] { launch_beta_planes(p, t, h->stream); });
         h->launch(kKRiskBaseline, [&] { launch_risk_baseline(p, t, h->stream); });
+        if (p.select_prep) h->prep_t = t;
       }
       break;
     case 3: {
+      if (p.select_prep && h->prep_t != t)
+        throw std::invalid_argument(
+            "stage 3 needs stage 2 of the same iteration after stage 1 (the risk launch sorts the residuals and "
+            "forms the cost norms: select_prep; MPCMMD_SELECT_PREP=0 moves them back to stages 1 and 3)");
       const int kind = ahead_kind(h), nxt = kind && t + 1 < h->T ? t + 1 : -1;
       h->launch(kKSelect, [&] { launch_select(p, t, h->stream, nxt, kind); });
       h->ahead_t = nxt;
@@ -1013,6 +1023,7 @@ int begin_impl(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t
     h->begun = true;
     h->last_t = -1;
     h->ahead_t = -1;
+    h->prep_t = -1;
     return MPCMMD_OK;
   });
 }
@@ -1198,6 +1209,18 @@ int mpcmmd_solve_batch(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const
 }
 
 int32_t mpcmmd_max_configs(mpcmmd_handle* h) { return h ? h->Gmax : 0; }
+
+int mpcmmd_handle_info(mpcmmd_handle* h, const char* name, int64_t* value) {
+  if (!h || !name || !value) return fail(MPCMMD_E_INVALID, "null argument");
+  const std::string k(name);
+  if (k == "gen_wave") *value = h->p.gen_wave ? 1 : 0;
+  else if (k == "select_prep") *value = h->prep_on && !h->carla && h->p.risk_rows ? 1 : 0;
+  else if (k == "fused_small") *value = h->fused_small ? 1 : 0;
+  else if (k == "groups") *value = h->groups;
+  else if (k == "capacity") *value = int64_t(h->Gmax) * h->B;
+  else return fail(MPCMMD_E_INVALID, "unknown handle_info name " + k);
+  return MPCMMD_OK;
+}
 
 int mpcmmd_carla_begin(mpcmmd_handle* h, int32_t cost_kind, int32_t idx_mpc, const float init_state[6],
                        const float mean[8], const float cov[64], const float* x_obs, const float* y_obs, float v_des,

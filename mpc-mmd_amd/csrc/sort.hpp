@@ -84,9 +84,14 @@ DEVI unsigned long long bitonic_reg_dpp(unsigned long long a, int N, unsigned lo
 // thread i, threads >= N hold ~0): every wave sorts its 64 keys (bitonic,
 // DPP / permlane moves), then runs of L = 64, 128, .. are merged pairwise --
 // a key's place in the merged run is its place in its own run plus the
-// number of smaller keys in the partner run (a binary search in LDS; keys are
-// distinct, so no ties), one barrier per level (k: 2 x 1024 words, the levels
-// alternate halves).  Returns a; idx = its position in the sorted order.
+// number of smaller keys in the partner run (a binary search in LDS; real
+// keys are distinct, so no ties), one barrier per level (k: 2 x 1024 words,
+// the levels alternate halves).  Returns a; idx = its position in the sorted
+// order.  The padding keys (~0, threads B..N-1) are equal, so a search would
+// give two pads of a pair of runs the same place and leave holes that a later
+// level reads; they instead keep idx = i at every level: after the wave sort
+// they sit at threads >= B, and the real keys of every merged pair of runs
+// fill exactly its slots below B, so the pads' own slots are the rest.
 DEVI unsigned long long merge_sort_reg(unsigned long long a, int& idx, int N, unsigned long long* k) {
   const int i = threadIdx.x, run = min(N, 64);
   for (int size = 2; size <= run; size <<= 1) a = wave_merge(a, size >> 1, size == run || (i & size) == 0);
@@ -96,7 +101,7 @@ DEVI unsigned long long merge_sort_reg(unsigned long long a, int& idx, int N, un
     unsigned long long* b = k + (lvl & 1) * 1024;
     if (i < N) b[idx] = a;
     __syncthreads();
-    if (i < N) {
+    if (i < N && a != ~0ull) {
       const int r = idx / L, pos = idx & (L - 1);
       const unsigned long long* part = b + (r ^ 1) * L;
       int base = 0;

@@ -18,7 +18,7 @@ COST = {"mmd_opt": 0, "mmd_random": 1, "cvar": 2, "saa": 3, "det": 4}  # det: CA
 NOISE = {"gaussian": 0, "beta": 1}
 VARIANT = {"static": 0, "dynamic": 1, "carla_town05": 2, "carla_town10hd": 3}
 RESULT_STRIDE_BETA_MAX = 32
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 SYMBOLS = (
     "mpcmmd_abi_version", "mpcmmd_last_error", "mpcmmd_device_count", "mpcmmd_create",
@@ -28,7 +28,7 @@ SYMBOLS = (
     "mpcmmd_host_constant", "mpcmmd_obs_dynamic_traj", "mpcmmd_validate", "mpcmmd_create_batch",
     "mpcmmd_max_configs", "mpcmmd_solve_batch", "mpcmmd_begin_batch", "mpcmmd_finish_batch",
     "mpcmmd_carla_begin", "mpcmmd_carla_solve", "mpcmmd_path_smoothing", "mpcmmd_path_parameters",
-    "mpcmmd_global_to_frenet", "mpcmmd_set_graphs",
+    "mpcmmd_global_to_frenet", "mpcmmd_set_graphs", "mpcmmd_handle_info",
 )
 
 
@@ -99,6 +99,7 @@ def lib():
     L.mpcmmd_create_batch.argtypes = [C.POINTER(Config), C.c_int32, C.POINTER(vp)]
     L.mpcmmd_max_configs.argtypes = [vp]
     L.mpcmmd_max_configs.restype = C.c_int32
+    L.mpcmmd_handle_info.argtypes = [vp, C.c_char_p, C.POINTER(C.c_int64)]
     ip = C.POINTER(C.c_int32)
     bargs = [vp, C.c_int32, C.c_int32, ip, fp, fp, fp, fp, fp, fp]
     L.mpcmmd_solve_batch.argtypes = bargs + [C.POINTER(Result)]
@@ -418,6 +419,13 @@ class Handle:
 
     def run_stage(self, stage, t):
         check(self._L.mpcmmd_run_stage(self._h, int(stage), int(t)))
+
+    def info(self, name):
+        """mpcmmd_handle_info: the handle's implementation choices ("gen_wave",
+        "select_prep", "fused_small", "groups", "capacity")."""
+        v = C.c_int64()
+        check(self._L.mpcmmd_handle_info(self._h, name.encode(), C.byref(v)))
+        return v.value
 
     # -- streams / profiling -----------------------------------------------------
     def set_stream(self, stream_ptr):

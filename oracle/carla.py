@@ -336,6 +336,36 @@ def compute_cost_carla(prob, cost_obs_w, cost_lane_w, cost_des_w, y, res, xd, yd
     return f32(tot)
 
 
+def plan_cost(prob, cost, cx, cy, steer, x_obs, y_obs, path, v_des):
+    """The CEM cost of ``Helper.compute_cost`` (C/opt/cem_helper.py:522-556)
+    evaluated on a returned plan (cx, cy, steering_best) as a noise-free
+    trajectory: the collision / lane / desired-lane bars of the nominal Frenet
+    path over the rollout horizon stand in for the risks (weighted as the
+    solve weights them, C/opt/cem.py:373-375), the projection residual is 0.
+    Test infrastructure: it ranks two solutions of the same problem (the
+    sensitivity-ensemble check of tests/test_gpu_carla.py), it is not a step of
+    the reference's algorithm."""
+    p = prob
+    Hh = p.num_prime
+    cx = np.asarray(cx, F32)[None]
+    cy = np.asarray(cy, F32)[None]
+    x = basis_eval(p.P, cx)
+    y = basis_eval(p.P, cy)
+    xd, yd = basis_eval(p.Pdot, cx), basis_eval(p.Pdot, cy)
+    xdd, ydd = basis_eval(p.Pddot, cx), basis_eval(p.Pddot, cy)
+    arc = np.asarray(path["arc_vec"], F32)
+    kap = interp(np.clip(x, F32(0), arc[-1]), arc, path["kappa"])
+    xs, ys = x[:, None, :Hh], y[:, None, :Hh]
+    cb = C.compute_f_bar_max(p, xs, ys, np.asarray(x_obs, F32)[:, :Hh], np.asarray(y_obs, F32)[:, :Hh])[:, 0]
+    lb, ub = C.lane_bar_max(p, ys)
+    des = lane_des_bar(p, ys)[:, 0]
+    w_obs, w_lane, w_des = {"mmd_opt": (p.weight_mmd_obs, p.weight_mmd_lane, p.weight_mmd_lane_des)}.get(
+        cost, (p.weight_cvar_obs, p.weight_cvar_lane, p.weight_cvar_lane_des))
+    tot = compute_cost_carla(p, F32(w_obs) * cb, F32(w_lane) * (lb[:, 0] + ub[:, 0]), F32(w_des) * des, y,
+                             np.zeros(1, F32), xd, yd, xdd, ydd, F32(v_des), np.asarray(steer, F32)[None], kap)
+    return float(tot[0])
+
+
 class CarlaDraws:
     """``rng.Draws`` plus the noisy-initial-state normals ``init_eps``
     [R, 4] (``C/opt/cem_helper.py:665``: MVN(0, I_4) = standard normals; R =
@@ -519,17 +549,30 @@ class CarlaCEM(CEM):
         return out, info
 
     def solve_carla(self, cost, idx_mpc, init_state, mean, cov, x_obs, y_obs, v_des, path, draws, trace=None,
-                    iters=None):
+                    iters=None, start=None, perturb=None, snapshots=None):
         """compute_cem_mmd / compute_cem_cvar (C/opt/cem.py:217-441, 444-629).
-        Returns (cx, cy, v_best [100], steering [100], mean_param [8])."""
+        Returns (cx, cy, v_best [100], steering [100], mean_param [8]).
+
+        Test hooks (none changes the algorithm): ``snapshots`` (a list)
+        receives a copy of the carry before every iteration; ``start`` = (t0,
+        carry) resumes from such a copy at iteration t0; ``perturb(t, obs, lane,
+        des)`` may replace an iteration's risks before the elite selection (the
+        sensitivity ensembles of tests/test_gpu_carla.py)."""
         p = self.prob
         x_obs = np.asarray(x_obs, F32)
         y_obs = np.asarray(y_obs, F32)
-        st = self.init_carla(cost, init_state, mean, cov, path, draws)
+        if start is None:
+            t0, st = 0, self.init_carla(cost, init_state, mean, cov, path, draws)
+        else:
+            t0, st = start[0], {k: np.array(v, copy=True) for k, v in start[1].items()}
         out = None
-        for t in range(p.maxiter_cem if iters is None else iters):
+        for t in range(t0, p.maxiter_cem if iters is None else iters):
+            if snapshots is not None:
+                snapshots.append({k: np.array(v, copy=True) for k, v in st.items()})
             pr, acc, steer = self.front_carla(st, path)
             obs, lane, des, extra = self.candidate_costs_carla(cost, st, acc, steer, x_obs, y_obs, path, draws, t)
+            if perturb is not None:
+                obs, lane, des = perturb(t, obs, lane, des)
             out, info = self.select_carla(cost, st, t, pr, steer, obs, lane, des, F32(v_des), draws, extra)
             if trace is not None:
                 trace.append(dict(res_norm=pr["res_norm"], obs=obs, lane=lane, des=des, steer=steer,
