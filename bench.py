@@ -414,10 +414,14 @@ def _carla_modules():
 def run_carla(ticks, warmup, local, n=None):
     """Per-tick time of the CARLA loop body on replayed ticks
     (carla/main_carla.py:345-382): the path / obstacle preprocessing through
-    the drop-in's helpers, then compute_cem_mmd and compute_cem_cvar, each
-    carrying its own mean_param to the next tick (:378).  Wall-clock per
-    tick (synchronous calls, as the driver makes them), against the 50 ms
-    tick of carla_simulation.py:20."""
+    the drop-in's helpers, then the solve.  The reference's driver runs ONE
+    cost per tick (``--costs`` picks func_cem = compute_cem_mmd, _cvar or _det,
+    main_carla.py:188-194, called at :378-382), so a tick of cost c is the
+    preprocessing + that solve, each cost carrying its own mean_param to the
+    next tick (:378); wall clock (synchronous calls, as the driver makes
+    them) against the 50 ms tick of carla_simulation.py:20.  The three solves
+    are timed on the same ticks, back to back; "ms_per_tick_mmd_plus_cvar" is
+    the stricter mmd + cvar sum earlier rounds reported."""
     import torch
     w = dict(CARLA_WORKLOAD)
     if n is not None:
@@ -482,11 +486,16 @@ def run_carla(ticks, warmup, local, n=None):
             conc.append(time.perf_counter() - t0)
     conc = np.array(conc) * 1e3
     desc = w["desc"].format(n=w["num_reduced"], M=w["num_reduced"] ** 2)
+    tick = {c: a[:, 0] + a[:, j] for c, j in (("mmd_opt", 1), ("cvar", 2), ("det", 4))}
+    per_cost = {c: {"ms_per_tick": float(np.mean(v)), "median_ms_per_tick": float(np.median(v)),
+                    "p90_ms_per_tick": float(np.percentile(v, 90)),
+                    "ticks_within_budget": float(np.mean(v <= w["budget_ms"]))} for c, v in tick.items()}
     return {"baseline": w["baseline"], "workload": desc, "num_reduced_set": w["num_reduced"], "ticks": ticks,
-            "value": 1e3 / float(np.mean(a[:, 3])), "unit": "ticks/s",
-            "ms_per_tick": float(np.mean(a[:, 3])), "median_ms_per_tick": float(np.median(a[:, 3])),
-            "p90_ms_per_tick": float(np.percentile(a[:, 3], 90)), "budget_ms": w["budget_ms"],
-            "ticks_within_budget": float(np.mean(a[:, 3] <= w["budget_ms"])),
+            "value": 1e3 / per_cost["mmd_opt"]["ms_per_tick"], "unit": "ticks/s (--costs mmd_opt)",
+            "tick": "main_carla.py:188-194: one cost per tick = preprocessing + that solve",
+            "per_cost": per_cost, "budget_ms": w["budget_ms"],
+            "ms_per_tick_mmd_plus_cvar": float(np.mean(a[:, 3])),
+            "ticks_within_budget_mmd_plus_cvar": float(np.mean(a[:, 3] <= w["budget_ms"])),
             "ms_preprocess": float(np.mean(a[:, 0])), "ms_mmd": float(np.mean(a[:, 1])),
             "ms_cvar": float(np.mean(a[:, 2])),
             "ms_det": float(np.mean(a[:, 4])), "median_ms_det": float(np.median(a[:, 4])),
@@ -518,8 +527,8 @@ def main():
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world} (launch N>1 with torchrun)")
     torch.cuda.set_device(local)
     if a.workload == "carla":  # configs[4] alone (one GPU, a real-time tick loop: no sharding)
-        print(json.dumps({"metric": "CARLA ticks/s (mmd_opt + cvar per tick)", **run_carla(a.steps, a.warmup, local, n=a.carla_n)}),
-              flush=True)
+        print(json.dumps({"metric": "CARLA ticks/s (one compute_cem_* per tick, main_carla.py:188-194)",
+                          **run_carla(a.steps, a.warmup, local, n=a.carla_n)}), flush=True)
         return
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))

@@ -1689,6 +1689,7 @@ DEVI void bdirect_body(const Params& p, int tb, int split, int lpt, int cand, in
   const int s_lo = first_sample(tb);
   const int i_lo = s_lo * n, i_hi = kBetaSamples * n;
   const int32_t* gsel = p.bsel + size_t(b) * kBetaSamples * n;
+  MPCMMD_STAMPW(p, 5);
   // direct pairs keep their row; the others get row -1
   for (int i = i_lo + tid; i < i_hi; i += NT) sl[i] = dflag[i] ? short(gsel[i]) : short(-1);
   for (int s = s_lo + tid; s < kBetaSamples; s += NT) csg[s] = kNegLog2e / p.bsig[size_t(b) * kBetaSamples + s];
@@ -1773,6 +1774,7 @@ DEVI void bdirect_body(const Params& p, int tb, int split, int lpt, int cand, in
   }
   __syncthreads();
   MPCMMD_STAMP(p, 19);
+  MPCMMD_STAMPW(p, 6);
   const float4* Dg = reinterpret_cast<const float4*>(p.bdist + size_t(b) * M * Md);
   // this part's rows order[part + split q], q from the workgroup's counter
   // (U: past the end)
@@ -1849,6 +1851,7 @@ DEVI void bdirect_body(const Params& p, int tb, int split, int lpt, int cand, in
     }
   }
   MPCMMD_STAMP(p, 20);
+  MPCMMD_STAMPW(p, 7);
 }
 
 #ifndef MPCMMD_FUSED_TU
@@ -3206,18 +3209,18 @@ int ker_split(int nb, int target) {
 
 void launch_bkernel(const Params& p, int tb, hipStream_t s) {
   const size_t sc = ker_scratch(p.M, p.n, tb);
-  hipLaunchKernelGGL(k_bkernel, dim3(p.nb * ker_split(p.nb, 512)), dim3(64 * kKerWaves), ker_lds(p.M, p.n, sc).total, s,
-                     p, tb, ker_split(p.nb, 512), int(sc));
+  hipLaunchKernelGGL(k_bkernel, dim3(p.nb * ker_split(p.nb, p.ker_target)), dim3(64 * kKerWaves),
+                     ker_lds(p.M, p.n, sc).total, s, p, tb, ker_split(p.nb, p.ker_target), int(sc));
 }
 
 template <int NV4>
 void launch_bdirect_v(const Params& p, int tb, int split, hipStream_t s) {
   hipLaunchKernelGGL((k_bdirect<NV4>), dim3(p.nb * split), dim3(64 * kDirWaves), dir_lds(p.M, p.n).total, s, p, tb,
-                     ker_split(p.nb, 512), split, 1);
+                     ker_split(p.nb, p.ker_target), split, 1);
 }
 
 void launch_bdirect(const Params& p, int tb, hipStream_t s) {
-  const int split = ker_split(p.nb, 2048);
+  const int split = ker_split(p.nb, p.dir_target);
   switch (dist_stride(p.M) >> 8) {
 #define MPCMMD_KER_CASE(V) \
   case V:                  \

@@ -101,6 +101,8 @@ struct Params {
   int32_t select_prep;     // the risk launch also sorts the residuals and forms the cost norms (cost.hpp)
   int32_t beta_dump;       // fused rollouts also store their Beta draws in bplane (MPCMMD_BETA_DUMP, tests)
   int32_t risk_rows;       // 1 (default): the row-lane rollouts over Beta planes; 0: fused (MPCMMD_RISK_FUSED=1)
+  int32_t ker_target;      // k_bkernel parts: enough for this many workgroups per launch (default 512)
+  int32_t dir_target;      // k_bdirect parts: enough for this many workgroups per launch (default 2048)
   int32_t gen_wave;        // 1: beta-CEM generators by k_bgen_wave (a wave per block: the latency-bound small
                            // batches, Bt <= 512); 0: k_bgen (a quad per block: throughput). Fixed per handle.
   const float* beta_z0;    // [100][M+1]

@@ -738,6 +738,10 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     // the batch is split into groups or whether k_bcem_small runs it
     p.gen_wave = BT <= 512 && h->n <= 24;
     if (const char* g = std::getenv("MPCMMD_GENWAVE")) p.gen_wave = std::atoi(g) != 0;
+    p.ker_target = 512;
+    p.dir_target = 2048;
+    if (const char* g = std::getenv("MPCMMD_KER_TARGET")) p.ker_target = std::max(1, std::atoi(g));
+    if (const char* g = std::getenv("MPCMMD_DIR_TARGET")) p.dir_target = std::max(1, std::atoi(g));
     if (const char* g = std::getenv("MPCMMD_BETA_DUMP")) p.beta_dump = std::atoi(g) != 0;
     p.risk_rows = 1;  // the row-lane path is the faster one at configs[2]; MPCMMD_RISK_FUSED=1: fused
     if (const char* g = std::getenv("MPCMMD_RISK_FUSED")) p.risk_rows = std::atoi(g) == 0;

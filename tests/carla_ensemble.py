@@ -14,7 +14,7 @@ of the members' returned tuples is the oracle's own sensitivity to an ulp at
 that point.
 
 Members run in child processes (spawn: a fresh interpreter that imports only
-NumPy and oracle/, never HIP), all eight at once (the GPU box gives a job 16
+NumPy and oracle/, never HIP), eight at a time (the GPU box gives a job 16
 CPUs).
 """
 import concurrent.futures as cf
@@ -58,7 +58,7 @@ def _member(args):
 _ONE_THREAD = ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")
 
 
-def run(shape, inputs, tp, snap, members=8, workers=8):
+def run(shape, inputs, tp, snap, members=16, workers=8):
     """shape = (n, B, H, O, T, level, town, idx, draw_seed); inputs = (init,
     xo, yo, path).  Returns the members' result dicts.  The children's BLAS
     runs single-threaded (each member already spreads its beta-CEMs over a

@@ -336,7 +336,7 @@ def test_carla_mmd_free_run(native, tick, town):
     oracle's), and it is reported.  Without a parting the returned (cx, cy,
     v_best, steering, mean_param) must agree within 1e-4.  After a parting the
     bound is the oracle's own sensitivity at that point (tests/carla_ensemble.py):
-    eight oracle runs resume from the oracle's carry at the parting iteration
+    sixteen oracle runs resume from the oracle's carry at the parting iteration
     with that iteration's risks shifted by 1-2 ulp per candidate (the size of
     the GPU-vs-oracle difference).  Per returned quantity the GPU's distance
     from the oracle must be within 1.25 x the ensemble's diameter, and its
