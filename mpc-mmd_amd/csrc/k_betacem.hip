@@ -183,6 +183,7 @@ constexpr int kDistThreads = 256;
 // the candidate's column features (42 KB) are read from HBM once and then
 // hit that XCD's L2, instead of once per tile.
 constexpr int kXcds = 8;
+constexpr int kCUs = 256;  // MI355X compute units (launch sizing only)
 
 // The matrix is symmetric and |a - b| == |b - a| exactly, so a tile of rows
 // computes only the columns from its own first row on and also writes the
@@ -1219,6 +1220,8 @@ __global__ __launch_bounds__(64) void k_bselect(Params p, int tb) {
   __shared__ __attribute__((aligned(16))) unsigned long long cand[64 * R + 8];
   __shared__ __attribute__((aligned(16))) uint32_t lm[64];
   __shared__ int scratch[128];
+  // this beta-iteration's direct-pair list starts empty (k_bkernel appends)
+  if (blockIdx.y == 0 && tidx() == 0) p.bdlcount[size_t(p.b0 + blockIdx.x) * kBetaIters + tb] = 0;
   bselect_wave<NQ, R, G>(p, tb, p.b0 + blockIdx.x, blockIdx.y, gridDim.y, cand, lm, scratch);
 }
 #endif
@@ -1388,7 +1391,7 @@ static_assert(kMomR == 12 && kMom == 12, "record layout: P_0..P_11 in float4s 0.
 // mom_l / feat_l: LDS copies of the candidate's series records and feature
 // rows (k_bcem_small, which keeps them for its 20 beta-iterations), else null
 // (read from global memory)
-template <int NW>
+template <int NW, bool kList = false>
 DEVI void bkernel_body(const Params& p, int tb, int cand, int part, int split, int scratch, char* smem,
                        const float4* mom_l = nullptr, const float4* feat_l = nullptr) {
   constexpr int kKerWaves = NW;
@@ -1478,6 +1481,10 @@ DEVI void bkernel_body(const Params& p, int tb, int cand, int part, int split, i
       const bool direct = !series && tb > 0;  // first iteration: k_bmoment summed them
       dflag[i] = direct ? 1 : 0;
       nd += direct ? 1 : 0;
+      if (kList && direct) {  // k_bdirect_pairs' list (its order is free: every pair's sum is its own)
+        const int at = atomicAdd(&p.bdlcount[size_t(b) * kBetaIters + tb], 1);
+        if (at < kBetaSamples * n) p.bdlist[size_t(b) * kBetaSamples * n + at] = i;
+      }
     }
     nd = wave_total(nd);
     if (lane == 0) atomicAdd(&misc[2], nd);
@@ -1648,10 +1655,11 @@ DEVI void bkernel_body(const Params& p, int tb, int cand, int part, int split, i
 // two workgroups per CU: 8 waves per SIMD, which needs <= 64 VGPRs and <= 80
 // SGPRs (MI355X_MICROARCH.md residency rules: 90 SGPRs admitted one)
 #ifndef MPCMMD_FUSED_TU
+template <bool kList>
 __global__ __launch_bounds__(64 * kKerWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_bkernel(Params p, int tb, int split, int scratch) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int cand = blockIdx.x / split, part = blockIdx.x - cand * split;
-  bkernel_body<kKerWaves>(p, tb, cand, part, split, scratch, smem);
+  bkernel_body<kKerWaves, kList>(p, tb, cand, part, split, scratch, smem);
 }
 #endif
 
@@ -1855,13 +1863,87 @@ DEVI void bdirect_body(const Params& p, int tb, int split, int lpt, int cand, in
 }
 
 #ifndef MPCMMD_FUSED_TU
-template <int NV4>
-__global__ __launch_bounds__(64 * kDirWaves) void k_bdirect(Params p, int tb, int kparts, int split, int lpt) {
+template <int NV4, int NW>
+__global__ __launch_bounds__(64 * NW) void k_bdirect(Params p, int tb, int kparts, int split, int lpt) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int cand = blockIdx.x / split, part = blockIdx.x - cand * split;
   const int total = bdirect_total(p, p.b0 + cand, kparts);
   if (total == 0) return;  // block-uniform
-  bdirect_body<NV4, kDirWaves>(p, tb, split, lpt, cand, part, total, smem);
+  bdirect_body<NV4, NW>(p, tb, split, lpt, cand, part, total, smem);
+}
+
+// k_bdirect_pairs: the same row sums from k_bkernel's list of flagged pairs,
+// no per-candidate setup (k_bdirect counting-sorts the pairs by mother row in
+// LDS first, which at the reference's num_batch = 100 -- CARLA, where a few
+// percent of all pairs are direct at every beta-iteration -- costs more than
+// the sums).  A wave takes PJ listed pairs, issues all their distance-row
+// loads (lane L: float4s L + 64 t of row sel[i]) before the first
+// exponential, forms each pair's per-lane terms exactly as bdirect_body's
+// do_row (packed scale, v_exp_f32, the same pairwise order), and reduces the
+// PJ slots by one transpose_sum8, whose tree is the same for every slot: the
+// bits of k_bdirect.  Workgroups: (candidate, part), kDirWaves waves each.
+template <int NV4, int PJ>
+__global__ __launch_bounds__(64 * kDirWaves) void k_bdirect_pairs(Params p, int tb, int parts) {
+  static_assert(PJ >= 1 && PJ <= 8, "pairs per wave");
+  // a candidate's parts on blocks of one blockIdx % 8 (one XCD under the
+  // observed round-robin dispatch, for L2 reuse of its distance rows; any
+  // placement is correct): the grid is a multiple of 8, its block L of XCD
+  // group x = blockIdx % 8 is the (x * grid / 8 + blockIdx / 8)-th (cand, part)
+  const int per = gridDim.x >> 3, L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  const int cand = L / parts, part = L - cand * parts;
+  if (cand >= p.nb) return;
+  const int b = p.b0 + cand, M = p.M, n = p.n, Md = dist_stride(M);
+  const int lane = tidx() & 63, w = __builtin_amdgcn_readfirstlane(int(tidx()) >> 6);
+  const int cnt = min(p.bdlcount[size_t(b) * kBetaIters + tb], kBetaSamples * n);
+  const int groups = (cnt + PJ - 1) / PJ, nw = parts * kDirWaves;
+  if (part * kDirWaves >= groups) return;  // block-uniform
+  const int32_t* list = p.bdlist + size_t(b) * kBetaSamples * n;
+  const int32_t* gsel = p.bsel + size_t(b) * kBetaSamples * n;
+  const float* gsig = p.bsig + size_t(b) * kBetaSamples;
+  float* rowsum = p.brow + size_t(b) * kBetaSamples * n;
+  const float4* Dg = reinterpret_cast<const float4*>(p.bdist + size_t(b) * M * Md);
+  if (part == 0 && tidx() == 0) atomicAdd(&p.stats[1], static_cast<unsigned long long>(cnt));
+  for (int g = part * kDirWaves + w; g < groups; g += nw) {
+    int pi[PJ];
+    float cs[PJ];
+    float4 x[PJ][NV4];
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {  // a past-the-end slot repeats the group's first pair (not stored)
+      const int k = g * PJ + j < cnt ? g * PJ + j : g * PJ;
+      pi[j] = list[k];
+    }
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+      const float4* src = Dg + size_t(gsel[pi[j]]) * (Md >> 2) + lane;
+#pragma unroll
+      for (int t = 0; t < NV4; ++t) x[j][t] = src[64 * t];
+      cs[j] = kNegLog2e / gsig[pi[j] / n];
+    }
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.0f;
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+      const f2 c2 = {cs[j], cs[j]};
+      f2 a0, a1;
+#pragma unroll
+      for (int t = 0; t < NV4; ++t) {
+        const f2 t0 = f2{x[j][t].x, x[j][t].y} * c2, t1 = f2{x[j][t].z, x[j][t].w} * c2;
+        const f2 e0 = {__builtin_amdgcn_exp2f(t0.x), __builtin_amdgcn_exp2f(t0.y)};
+        const f2 e1 = {__builtin_amdgcn_exp2f(t1.x), __builtin_amdgcn_exp2f(t1.y)};
+        a0 = t == 0 ? e0 : a0 + e0;
+        a1 = t == 0 ? e1 : a1 + e1;
+      }
+      a0 += a1;
+      v[j] = a0.x + a0.y;
+    }
+    const float sum = transpose_sum8(v);  // slot j's total in lanes 8 j + 4..7
+    const int j = lane >> 3;
+    int pj = pi[0];
+#pragma unroll
+    for (int q = 1; q < PJ; ++q) pj = j == q ? pi[q] : pj;
+    if ((lane & 7) == 4 && j < PJ && g * PJ + j < cnt) rowsum[pj] = sum;
+  }
 }
 #endif
 
@@ -3131,11 +3213,13 @@ void launch_bsel0(const Params& p, hipStream_t s) {
   hipLaunchKernelGGL(k_bsel0, dim3(unsigned(std::min<size_t>((total + 255) / 256, 4096))), dim3(256), 0, s, p);
 }
 
-int sel_waves(int nb) { return std::max(4, std::min(16, 16384 / std::max(1, nb))); }
+// (small launches, nb <= 128: up to Params::sel_cap waves per candidate --
+// CARLA n = 22, B = 100: 16 -> 64 took 1.5 ms off a 49.5 ms solve)
+int sel_waves(int nb, int cap) { return std::max(4, std::min(nb <= 128 ? cap : 16, 16384 / std::max(1, nb))); }
 
 template <int NQ>
 void launch_bselect_q(const Params& p, int tb, hipStream_t s) {
-  const dim3 grid(p.nb, sel_waves(p.nb));
+  const dim3 grid(p.nb, sel_waves(p.nb, p.sel_cap));
   if (p.n <= 24)
     hipLaunchKernelGGL((k_bselect<NQ, 1, 32>), grid, dim3(64), 0, s, p, tb);
   else if (p.n <= 48)
@@ -3172,7 +3256,9 @@ void launch_bselect(const Params& p, int tb, hipStream_t s) {
 
 template <int NP>
 void launch_bqp_quad(const Params& p, int tb, int qps, hipStream_t s) {
-  constexpr int T = qp_threads(NP);
+  // threads per workgroup: qp_threads, or 64 (16 QPs) where the launch
+  // would give the CUs barely one workgroup each (Params::qp_small)
+  const int T = p.qp_small && (qps + 31) / 32 < 2 * kCUs ? 64 : qp_threads(NP);
   const size_t lds = (size_t(T / 4) * tri_stride(p.n) + kQpZeros) * 4;
   hipLaunchKernelGGL((k_bqp<NP>), dim3((qps * 4 + T - 1) / T), dim3(T), lds, s, p, tb);
 }
@@ -3207,19 +3293,60 @@ int ker_split(int nb, int target) {
   return split;
 }
 
+// k_bdirect_pairs (and k_bkernel's pair list) for launches of <= 256
+// candidates: at B = 100 the row-sorted k_bdirect's per-candidate setup
+// dominates; at B = 1024 (few direct pairs) the list's atomics cost k_bkernel
+// more than they save (mmd_opt 133 -> 129 steps/s), so k_bdirect stays there
+bool use_pairs(const Params& p) { return p.dir_pairs && p.nb <= 256; }
+
 void launch_bkernel(const Params& p, int tb, hipStream_t s) {
   const size_t sc = ker_scratch(p.M, p.n, tb);
-  hipLaunchKernelGGL(k_bkernel, dim3(p.nb * ker_split(p.nb, p.ker_target)), dim3(64 * kKerWaves),
-                     ker_lds(p.M, p.n, sc).total, s, p, tb, ker_split(p.nb, p.ker_target), int(sc));
+  const dim3 grid(p.nb * ker_split(p.nb, p.ker_target)), block(64 * kKerWaves);
+  const size_t lds = ker_lds(p.M, p.n, sc).total;
+  if (use_pairs(p))
+    hipLaunchKernelGGL(k_bkernel<true>, grid, block, lds, s, p, tb, ker_split(p.nb, p.ker_target), int(sc));
+  else
+    hipLaunchKernelGGL(k_bkernel<false>, grid, block, lds, s, p, tb, ker_split(p.nb, p.ker_target), int(sc));
 }
 
 template <int NV4>
 void launch_bdirect_v(const Params& p, int tb, int split, hipStream_t s) {
-  hipLaunchKernelGGL((k_bdirect<NV4>), dim3(p.nb * split), dim3(64 * kDirWaves), dir_lds(p.M, p.n).total, s, p, tb,
-                     ker_split(p.nb, p.ker_target), split, 1);
+  if (p.dir_waves >= 16)
+    hipLaunchKernelGGL((k_bdirect<NV4, 16>), dim3(p.nb * split), dim3(64 * 16), dir_lds(p.M, p.n).total, s, p, tb,
+                       ker_split(p.nb, p.ker_target), split, 1);
+  else if (p.dir_waves >= 8)
+    hipLaunchKernelGGL((k_bdirect<NV4, 8>), dim3(p.nb * split), dim3(64 * 8), dir_lds(p.M, p.n).total, s, p, tb,
+                       ker_split(p.nb, p.ker_target), split, 1);
+  else
+    hipLaunchKernelGGL((k_bdirect<NV4, kDirWaves>), dim3(p.nb * split), dim3(64 * kDirWaves), dir_lds(p.M, p.n).total,
+                       s, p, tb, ker_split(p.nb, p.ker_target), split, 1);
+}
+
+// pairs per wave of k_bdirect_pairs: as many distance rows in flight as fit
+// ~64 VGPRs of operands (NV4 float4s per lane and row)
+template <int NV4>
+void launch_bdirect_pairs_v(const Params& p, int tb, hipStream_t s) {
+  constexpr int PJ = NV4 <= 2 ? 8 : (NV4 <= 4 ? 4 : (NV4 <= 8 ? 2 : 1));
+  const int parts = std::max(1, std::min(64, (p.dir_target + p.nb - 1) / p.nb));
+  const int grid = (p.nb * parts + 7) & ~7;
+  hipLaunchKernelGGL((k_bdirect_pairs<NV4, PJ>), dim3(grid), dim3(64 * kDirWaves), 0, s, p, tb, parts);
 }
 
 void launch_bdirect(const Params& p, int tb, hipStream_t s) {
+  if (use_pairs(p)) {
+    switch (dist_stride(p.M) >> 8) {
+#define MPCMMD_PAIR_CASE(V) \
+  case V:                   \
+    return launch_bdirect_pairs_v<V>(p, tb, s);
+      MPCMMD_PAIR_CASE(1) MPCMMD_PAIR_CASE(2) MPCMMD_PAIR_CASE(3) MPCMMD_PAIR_CASE(4)
+      MPCMMD_PAIR_CASE(5) MPCMMD_PAIR_CASE(6) MPCMMD_PAIR_CASE(7) MPCMMD_PAIR_CASE(8)
+      MPCMMD_PAIR_CASE(9) MPCMMD_PAIR_CASE(10) MPCMMD_PAIR_CASE(11) MPCMMD_PAIR_CASE(12)
+      MPCMMD_PAIR_CASE(13) MPCMMD_PAIR_CASE(14) MPCMMD_PAIR_CASE(15)
+      default:
+        return launch_bdirect_pairs_v<16>(p, tb, s);
+#undef MPCMMD_PAIR_CASE
+    }
+  }
   const int split = ker_split(p.nb, p.dir_target);
   switch (dist_stride(p.M) >> 8) {
 #define MPCMMD_KER_CASE(V) \

@@ -101,6 +101,12 @@ struct Params {
   int32_t select_prep;     // the risk launch also sorts the residuals and forms the cost norms (cost.hpp)
   int32_t beta_dump;       // fused rollouts also store their Beta draws in bplane (MPCMMD_BETA_DUMP, tests)
   int32_t risk_rows;       // 1 (default): the row-lane rollouts over Beta planes; 0: fused (MPCMMD_RISK_FUSED=1)
+  int32_t* bdlist;         // [Bt][100 n] the flagged (direct) pairs of a beta-iteration, appended by k_bkernel
+  int32_t* bdlcount;       // [Bt][20] their count per beta-iteration (zeroed by k_bselect of that iteration)
+  int32_t dir_pairs;       // 1: k_bdirect_pairs (a wave per 8 listed pairs); 0: k_bdirect (rows sorted in LDS)
+  int32_t qp_small;        // k_bqp at 64 threads (16 QPs) per workgroup for launches of < 2 workgroups per CU
+  int32_t sel_cap;         // k_bselect: at most this many single-wave workgroups per candidate (default 16)
+  int32_t dir_waves;       // waves per k_bdirect workgroup (4, 8 or 16)
   int32_t ker_target;      // k_bkernel parts: enough for this many workgroups per launch (default 512)
   int32_t dir_target;      // k_bdirect parts: enough for this many workgroups per launch (default 2048)
   int32_t gen_wave;        // 1: beta-CEM generators by k_bgen_wave (a wave per block: the latency-bound small

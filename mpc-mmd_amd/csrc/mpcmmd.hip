@@ -114,6 +114,7 @@ struct mpcmmd_handle {
   static constexpr int kMaxGroups = 4;
   int groups = 1;
   bool groups_forced = false;
+  int small_groups = 2;  // groups for launches of 64..256 candidates (MPCMMD_SMALL_GROUPS)
   hipStream_t gstream[kMaxGroups] = {};
   hipEvent_t gev_start = nullptr, gev_done[kMaxGroups] = {};
   // whole-solve graphs: mpcmmd_iterate(0, T) captured once per (cost, path
@@ -353,7 +354,8 @@ void run_beta_cem(mpcmmd_handle* h) {
   }
   // the default split applies to launches of >= 1024 candidates (a batch
   // handle may run fewer configurations than it holds); MPCMMD_GROUPS forces it
-  const int G = h->prof ? 1 : (B >= 1024 || h->groups_forced ? h->groups : 1);
+  const bool small = B >= 64 && B <= 256;
+  const int G = h->prof ? 1 : (B >= 1024 || h->groups_forced ? h->groups : (small ? std::min(h->groups, h->small_groups) : 1));
   if (G <= 1) {
     for (int tb = 0; tb < kBetaIters; ++tb) run_beta_iteration(h, h->p, tb, h->stream);
     return;
@@ -653,6 +655,8 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
       p.bmom = (float*)h->alloc("bmom", BT * M * kMomStride * 4);
       p.bdflag = (unsigned char*)h->alloc("bdflag", BT * kBetaSamples * n);
       p.bdcount = (int32_t*)h->alloc("bdcount", BT * kMaxSplit * 4);
+      p.bdlist = (int32_t*)h->alloc("bdlist", BT * kBetaSamples * h->n * 4);
+      p.bdlcount = (int32_t*)h->alloc("bdlcount", BT * kBetaIters * 4);
       p.sel0 = (const int32_t*)h->alloc("sel0", size_t(kBetaSamples) * n * 4);
       p.sig0 = (const float*)h->alloc("sig0", size_t(kBetaSamples) * 4);
       p.rp0 = (const int32_t*)h->alloc("rp0", (M + 1) * 4);
@@ -728,6 +732,10 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     // chip: one group's MFMA-bound sampler overlaps the other's VALU-bound
     // kernel sums (B = 1024: 82.2 -> 92.8 steps/s; four groups: 72.6)
     if (BT >= 1024) h->groups = 2;
+    // small batches on the per-iteration kernels (num_reduced > 16; CARLA n = 22 at
+    // B = 100): two groups as well, for launches of 64..256 candidates
+    if (const char* g = std::getenv("MPCMMD_SMALL_GROUPS")) h->small_groups = std::max(1, std::atoi(g));
+    if (BT >= 64 && BT <= 256) h->groups = std::max(h->groups, h->small_groups);
     h->groups_forced = std::getenv("MPCMMD_GROUPS") != nullptr;
     if (const char* g = std::getenv("MPCMMD_GRAPH")) h->graphs = std::atoi(g) != 0;
     if (const char* g = std::getenv("MPCMMD_AHEAD")) h->ahead_on = std::atoi(g) != 0;
@@ -738,7 +746,15 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     // the batch is split into groups or whether k_bcem_small runs it
     p.gen_wave = BT <= 512 && h->n <= 24;
     if (const char* g = std::getenv("MPCMMD_GENWAVE")) p.gen_wave = std::atoi(g) != 0;
-    p.ker_target = 512;
+    p.dir_pairs = 1;
+    if (const char* g = std::getenv("MPCMMD_DIR_PAIRS")) p.dir_pairs = std::atoi(g) != 0;
+    p.qp_small = 1;
+    if (const char* g = std::getenv("MPCMMD_QP_SMALL")) p.qp_small = std::atoi(g) != 0;
+    p.sel_cap = 64;
+    if (const char* g = std::getenv("MPCMMD_SEL_CAP")) p.sel_cap = std::max(1, std::atoi(g));
+    p.dir_waves = 4;
+    if (const char* g = std::getenv("MPCMMD_DIR_WAVES")) p.dir_waves = std::atoi(g);
+    p.ker_target = 128;  // parts per candidate only below 128 candidates per launch (B = 100: 8 -> 2 parts)
     p.dir_target = 2048;
     if (const char* g = std::getenv("MPCMMD_KER_TARGET")) p.ker_target = std::max(1, std::atoi(g));
     if (const char* g = std::getenv("MPCMMD_DIR_TARGET")) p.dir_target = std::max(1, std::atoi(g));

@@ -13,7 +13,7 @@ from parity import DEFAULT_COV, DEFAULT_INIT, DEFAULT_MEAN, make_pair
 pytestmark = pytest.mark.gpu
 
 
-def _run(native, monkeypatch, fused, cost, n, B, H, O, T, xo=None, yo=None, carla=None):
+def _run(native, monkeypatch, fused, cost, n, B, H, O, T, xo=None, yo=None, carla=None, keys=()):
     monkeypatch.setenv("MPCMMD_FUSED", "1" if fused else "0")
     if carla is None:
         ora, nat, xo_, yo_ = make_pair(native, cost, n=n, O=O, H=H, B=B, T=T)
@@ -29,7 +29,8 @@ def _run(native, monkeypatch, fused, cost, n, B, H, O, T, xo=None, yo=None, carl
     for t in range(T):
         nat.iterate(t, 1)
         nat.sync()
-        out.append({k: nat.read(k).copy() for k in ("beta", "sigma", "res_beta", "btrace", "obs_cost", "lane_cost")})
+        out.append({k: nat.read(k).copy() for k in ("beta", "sigma", "res_beta", "btrace", "obs_cost", "lane_cost")
+                    + tuple(keys)})
         out[-1]["tr"] = (nat.read("tr_proj", np.int32).copy(), nat.read("tr_obs", np.int32).copy(),
                          nat.read("tr_cem", np.int32).copy())
     res = nat.finish()
@@ -67,3 +68,35 @@ def test_fused_bits_carla(native, monkeypatch):
                 assert np.array_equal(got[t][k], ref[t][k], equal_nan=True), f"iteration {t}: {k} differs"
     for k in ("cx", "cy", "steering", "v_best", "mean_param"):
         assert np.array_equal(rg[k], rr[k]), k
+
+
+@pytest.mark.parametrize("case", ["static-22", "carla-22", "static-50"])
+def test_direct_pairs_same_bits(native, monkeypatch, case):
+    """k_bdirect_pairs (a wave per 8 listed direct pairs; MPCMMD_DIR_PAIRS=1,
+    the default) against k_bdirect (pairs counting-sorted by mother row in
+    LDS) on the per-iteration kernels: the same per-lane terms and the same
+    reduction tree for every slot, so the direct row sums (brow) and every
+    output carry the same bits."""
+    kind, n = case.split("-")
+    n = int(n)
+    T = 2
+    carla = None
+    B, H, O = (100, 30, 10) if n == 22 else (100, 20, 4)
+    if kind == "carla":
+        from test_gpu_carla import _tick
+        init, xo, yo, path = _tick(60, 3, 60)
+        carla = (init, xo, yo, path, "carla_town05")
+        H, O = 60, 3
+    runs = []
+    for pairs in ("0", "1"):
+        monkeypatch.setenv("MPCMMD_DIR_PAIRS", pairs)
+        runs.append(_run(native, monkeypatch, False, "mmd_opt", n, B, H, O, T, carla=carla, keys=("brow",)))
+    (ref, rr), (got, rg) = runs
+    for t in range(T):
+        for k in ref[t]:
+            if k == "tr":
+                assert all(np.array_equal(a, b) for a, b in zip(got[t][k], ref[t][k])), f"iteration {t}: elites"
+            else:
+                assert np.array_equal(got[t][k], ref[t][k], equal_nan=True), f"iteration {t}: {k} differs"
+    for k in ("cx", "cy"):
+        assert np.array_equal(np.asarray(rg[k]), np.asarray(rr[k])), k
