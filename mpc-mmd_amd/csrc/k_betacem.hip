@@ -1481,9 +1481,15 @@ DEVI void bkernel_body(const Params& p, int tb, int cand, int part, int split, i
       const bool direct = !series && tb > 0;  // first iteration: k_bmoment summed them
       dflag[i] = direct ? 1 : 0;
       nd += direct ? 1 : 0;
-      if (kList && direct) {  // k_bdirect_pairs' list (its order is free: every pair's sum is its own)
-        const int at = atomicAdd(&p.bdlcount[size_t(b) * kBetaIters + tb], 1);
-        if (at < kBetaSamples * n) p.bdlist[size_t(b) * kBetaSamples * n + at] = i;
+      if (kList) {  // the direct-pair list (its order is free: every pair's sum is its own)
+        const unsigned long long m = __ballot(direct);  // one atomic per wave
+        if (m) {
+          const int ld = __builtin_ctzll(m);
+          int at = 0;
+          if (lane == ld) at = atomicAdd(&p.bdlcount[size_t(b) * kBetaIters + tb], __popcll(m));
+          at = __shfl(at, ld, 64) + __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
+          if (direct && at < kBetaSamples * n) p.bdlist[size_t(b) * kBetaSamples * n + at] = i;
+        }
       }
     }
     nd = wave_total(nd);
@@ -1871,39 +1877,32 @@ __global__ __launch_bounds__(64 * NW) void k_bdirect(Params p, int tb, int kpart
   if (total == 0) return;  // block-uniform
   bdirect_body<NV4, NW>(p, tb, split, lpt, cand, part, total, smem);
 }
+#endif
 
-// k_bdirect_pairs: the same row sums from k_bkernel's list of flagged pairs,
-// no per-candidate setup (k_bdirect counting-sorts the pairs by mother row in
-// LDS first, which at the reference's num_batch = 100 -- CARLA, where a few
-// percent of all pairs are direct at every beta-iteration -- costs more than
-// the sums).  A wave takes PJ listed pairs, issues all their distance-row
-// loads (lane L: float4s L + 64 t of row sel[i]) before the first
-// exponential, forms each pair's per-lane terms exactly as bdirect_body's
-// do_row (packed scale, v_exp_f32, the same pairwise order), and reduces the
-// PJ slots by one transpose_sum8, whose tree is the same for every slot: the
-// bits of k_bdirect.  Workgroups: (candidate, part), kDirWaves waves each.
+// Direct row sums from k_bkernel's list of flagged pairs (k_bdirect_pairs),
+// no per-candidate setup (bdirect_body counting-sorts the
+// pairs by mother row in LDS first, which at the reference's num_batch = 100
+// -- CARLA, where about half of all pairs are direct at every beta-iteration
+// -- costs more than the sums).  A wave takes PJ listed pairs, issues all
+// their distance-row loads (lane L: float4s L + 64 t of row sel[i]) before the
+// first exponential, forms each pair's per-lane terms exactly as
+// bdirect_body's do_row (packed scale, v_exp_f32, the same pairwise order),
+// and reduces the PJ slots by one transpose_sum8, whose tree is the same for
+// every slot: the bits of bdirect_body.
+// Groups g0, g0 + gs, .. of PJ listed pairs of candidate b (cnt pairs) on the
+// calling wave.
 template <int NV4, int PJ>
-__global__ __launch_bounds__(64 * kDirWaves) void k_bdirect_pairs(Params p, int tb, int parts) {
+DEVI void direct_pairs_wave(const Params& p, int b, int cnt, int g0, int gs) {
   static_assert(PJ >= 1 && PJ <= 8, "pairs per wave");
-  // a candidate's parts on blocks of one blockIdx % 8 (one XCD under the
-  // observed round-robin dispatch, for L2 reuse of its distance rows; any
-  // placement is correct): the grid is a multiple of 8, its block L of XCD
-  // group x = blockIdx % 8 is the (x * grid / 8 + blockIdx / 8)-th (cand, part)
-  const int per = gridDim.x >> 3, L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-  const int cand = L / parts, part = L - cand * parts;
-  if (cand >= p.nb) return;
-  const int b = p.b0 + cand, M = p.M, n = p.n, Md = dist_stride(M);
-  const int lane = tidx() & 63, w = __builtin_amdgcn_readfirstlane(int(tidx()) >> 6);
-  const int cnt = min(p.bdlcount[size_t(b) * kBetaIters + tb], kBetaSamples * n);
-  const int groups = (cnt + PJ - 1) / PJ, nw = parts * kDirWaves;
-  if (part * kDirWaves >= groups) return;  // block-uniform
+  const int M = p.M, n = p.n, Md = dist_stride(M);
+  const int lane = tidx() & 63;
+  const int groups = (cnt + PJ - 1) / PJ;
   const int32_t* list = p.bdlist + size_t(b) * kBetaSamples * n;
   const int32_t* gsel = p.bsel + size_t(b) * kBetaSamples * n;
   const float* gsig = p.bsig + size_t(b) * kBetaSamples;
   float* rowsum = p.brow + size_t(b) * kBetaSamples * n;
   const float4* Dg = reinterpret_cast<const float4*>(p.bdist + size_t(b) * M * Md);
-  if (part == 0 && tidx() == 0) atomicAdd(&p.stats[1], static_cast<unsigned long long>(cnt));
-  for (int g = part * kDirWaves + w; g < groups; g += nw) {
+  for (int g = g0; g < groups; g += gs) {
     int pi[PJ];
     float cs[PJ];
     float4 x[PJ][NV4];
@@ -1944,6 +1943,29 @@ __global__ __launch_bounds__(64 * kDirWaves) void k_bdirect_pairs(Params p, int 
     for (int q = 1; q < PJ; ++q) pj = j == q ? pi[q] : pj;
     if ((lane & 7) == 4 && j < PJ && g * PJ + j < cnt) rowsum[pj] = sum;
   }
+}
+
+// pairs per wave of the pair-list direct sums: as many distance rows in flight
+// as fit ~64 VGPRs of operands (NV4 float4s per lane and row)
+HDI_CONST int direct_pj(int nv4) { return nv4 <= 2 ? 8 : (nv4 <= 4 ? 4 : (nv4 <= 8 ? 2 : 1)); }
+
+#ifndef MPCMMD_FUSED_TU
+// k_bdirect_pairs, workgroup = (candidate, part), kDirWaves waves each
+template <int NV4, int PJ>
+__global__ __launch_bounds__(64 * kDirWaves) void k_bdirect_pairs(Params p, int tb, int parts) {
+  // a candidate's parts on blocks of one blockIdx % 8 (one XCD under the
+  // observed round-robin dispatch, for L2 reuse of its distance rows; any
+  // placement is correct): the grid is a multiple of 8, its block L of XCD
+  // group x = blockIdx % 8 is the (x * grid / 8 + blockIdx / 8)-th (cand, part)
+  const int per = gridDim.x >> 3, L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  const int cand = L / parts, part = L - cand * parts;
+  if (cand >= p.nb) return;
+  const int b = p.b0 + cand, n = p.n;
+  const int w = __builtin_amdgcn_readfirstlane(int(tidx()) >> 6);
+  const int cnt = min(p.bdlcount[size_t(b) * kBetaIters + tb], kBetaSamples * n);
+  if (part * kDirWaves >= (cnt + PJ - 1) / PJ) return;  // block-uniform
+  if (part == 0 && tidx() == 0) atomicAdd(&p.stats[1], static_cast<unsigned long long>(cnt));
+  direct_pairs_wave<NV4, PJ>(p, b, cnt, part * kDirWaves + w, parts * kDirWaves);
 }
 #endif
 
@@ -3090,7 +3112,10 @@ __global__ __launch_bounds__(64 * W) void k_bcem_small(Params p0, int persist) {
     }
     __syncthreads();
     if (tb == 5) SMALL_STAMP(p, 2);
-    // K_mixed row sums and K_red (compute_beta.py:120-127)
+    // K_mixed row sums and K_red (compute_beta.py:120-127).  The direct sums
+    // by rows (bdirect_body): a candidate's direct pairs share its M rows
+    // several times over, and the pair-list form (direct_pairs_wave) measured
+    // no faster here (CARLA n = 10: 24.2 vs 24.3 ms per solve)
     bkernel_body<kSmallWaves>(p, tb, cand, 0, 1, int(ker_scratch(M, n, tb, kSmallWaves)), smem, mom_l, feat_l);
     __syncthreads();
     if (tb == 5) SMALL_STAMP(p, 3);
@@ -3322,11 +3347,9 @@ void launch_bdirect_v(const Params& p, int tb, int split, hipStream_t s) {
                        s, p, tb, ker_split(p.nb, p.ker_target), split, 1);
 }
 
-// pairs per wave of k_bdirect_pairs: as many distance rows in flight as fit
-// ~64 VGPRs of operands (NV4 float4s per lane and row)
 template <int NV4>
 void launch_bdirect_pairs_v(const Params& p, int tb, hipStream_t s) {
-  constexpr int PJ = NV4 <= 2 ? 8 : (NV4 <= 4 ? 4 : (NV4 <= 8 ? 2 : 1));
+  constexpr int PJ = direct_pj(NV4);
   const int parts = std::max(1, std::min(64, (p.dir_target + p.nb - 1) / p.nb));
   const int grid = (p.nb * parts + 7) & ~7;
   hipLaunchKernelGGL((k_bdirect_pairs<NV4, PJ>), dim3(grid), dim3(64 * kDirWaves), 0, s, p, tb, parts);

@@ -72,16 +72,17 @@ def test_fused_bits_carla(native, monkeypatch):
 
 @pytest.mark.parametrize("case", ["static-22", "carla-22", "static-50"])
 def test_direct_pairs_same_bits(native, monkeypatch, case):
-    """k_bdirect_pairs (a wave per 8 listed direct pairs; MPCMMD_DIR_PAIRS=1,
-    the default) against k_bdirect (pairs counting-sorted by mother row in
-    LDS) on the per-iteration kernels: the same per-lane terms and the same
-    reduction tree for every slot, so the direct row sums (brow) and every
-    output carry the same bits."""
-    kind, n = case.split("-")
+    """The direct row sums from k_bkernel's pair list (a wave per 8 listed
+    pairs; MPCMMD_DIR_PAIRS=1, the default: k_bdirect_pairs on the
+    per-iteration kernels of launches <= 256 candidates) against bdirect_body (pairs counting-sorted by mother row in
+    LDS): the same per-lane terms and the same reduction tree for every slot,
+    so the direct row sums (brow) and every output carry the same bits."""
+    kind, n = case.split("-")[:2]
+    fused = case.endswith("fused")
     n = int(n)
     T = 2
     carla = None
-    B, H, O = (100, 30, 10) if n == 22 else (100, 20, 4)
+    B, H, O = (100, 20, 4) if n == 50 else (100, 30, 10)
     if kind == "carla":
         from test_gpu_carla import _tick
         init, xo, yo, path = _tick(60, 3, 60)
@@ -90,7 +91,7 @@ def test_direct_pairs_same_bits(native, monkeypatch, case):
     runs = []
     for pairs in ("0", "1"):
         monkeypatch.setenv("MPCMMD_DIR_PAIRS", pairs)
-        runs.append(_run(native, monkeypatch, False, "mmd_opt", n, B, H, O, T, carla=carla, keys=("brow",)))
+        runs.append(_run(native, monkeypatch, fused, "mmd_opt", n, B, H, O, T, carla=carla, keys=("brow",)))
     (ref, rr), (got, rg) = runs
     for t in range(T):
         for k in ref[t]:
