@@ -135,6 +135,8 @@ struct mpcmmd_handle {
   // is k_risk_baseline (Params::select_prep); MPCMMD_SELECT_PREP=0: in
   // k_select / k_front
   bool prep_on = true;
+  // sampling_param's internal standard normals [B][8] (fixed key: every solve's)
+  std::vector<float> pop0_normals;
   // the iteration whose residual sort and cost norms the risk launch made
   // (-1: none since begin / the last front stage); stage 3 with select_prep
   // needs them for its own t
@@ -941,9 +943,11 @@ int begin_impl(mpcmmd_handle* h, int32_t n_cfg, int32_t cost_kind, const int32_t
     upload_staged(h, "idx_mpc", idx_mpc, size_t(G) * 4);
     upload_staged(h, "v_des", v_des, size_t(G) * 4);
     // sampling_param (cem_helper.py:122-150): fixed key, the same draws for every configuration
-    std::vector<float> z0;
-    if (draws && draws->pop0) z0.assign(draws->pop0, draws->pop0 + size_t(B) * 8);
-    else z0 = host_normals(kFixedKey0, h->cfg.seed, kStreamPop0, 0, size_t(B) * 8);
+    // (the internal draws depend on the seed and B only: made once per handle)
+    std::vector<float> z0x;
+    if (draws && draws->pop0) z0x.assign(draws->pop0, draws->pop0 + size_t(B) * 8);
+    else if (h->pop0_normals.empty()) h->pop0_normals = host_normals(kFixedKey0, h->cfg.seed, kStreamPop0, 0, size_t(B) * 8);
+    const std::vector<float>& z0 = draws && draws->pop0 ? z0x : h->pop0_normals;
     std::vector<double> sc(size_t(G) * 4 * kNvar, 0.0);
     std::vector<float> st0(size_t(G) * 8, 0.f), ob(size_t(G) * 2 * O * H), pop(size_t(G) * B * 8);
     std::vector<float> rows0;  // CARLA noisy initial rows [R0][8]
