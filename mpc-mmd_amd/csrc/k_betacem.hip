@@ -2114,6 +2114,22 @@ DEVI void bqp_solve(const Params& p, int b, int s, bool ok, const float* kr, con
     a2[t] = i < n ? 1.0f : 0.0f;
     rin[t] = 0.0f;
   }
+#if defined(MPCMMD_QP_VARIANT) && MPCMMD_QP_VARIANT >= 2
+  // PMC attribution builds (tools/qp_variants.sh; results are garbage):
+  // 2 = staging + the row loads only, 3 = staging only
+  {
+    float acc = 0.0f;
+#if MPCMMD_QP_VARIANT == 2
+#pragma unroll
+    for (int t = 0; t < T4; ++t)
+#pragma unroll
+      for (int k = 0; k < NP; ++k)
+        if (k <= 4 * t + 3) acc += A[t][k];
+#endif
+    if (ok && acc == 12345.0f) p.bcost[size_t(b) * kBetaSamples + s] = acc;
+    return;
+  }
+#endif
   // C in place: strict lower part from K_red, the diagonal 1.05 (1 for the
   // padding rows), entries above the diagonal 0
 #pragma unroll
@@ -2203,6 +2219,11 @@ DEVI void bqp_solve(const Params& p, int b, int s, bool ok, const float* kr, con
   float bf[T4];
 #pragma unroll
   for (int t = 0; t < T4; ++t) bf[t] = 4 * t + q < n ? a1[t] : 0.0f;
+#if defined(MPCMMD_QP_VARIANT) && MPCMMD_QP_VARIANT == 1
+  // PMC attribution build: no cost phase (the K_red re-read)
+  if (ok && q == 0) p.bcost[size_t(b) * kBetaSamples + s] = bf[0];
+  return;
+#endif
   // cost = beta^T K beta - 2 g^T beta in fp64, K = K_red re-read (unit
   // diagonal): r_i = sum_{k<i} K_ik beta_k by columns k, column k + 1's
   // entries in flight while column k is summed (two columns live, not the
