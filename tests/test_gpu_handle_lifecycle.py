@@ -73,3 +73,30 @@ def test_front_stage_after_create(native, shape):
     close("cx", nat.read("cx").reshape(B, 11), pr["c_x"], atol=1e-4)
     close("cy", nat.read("cy").reshape(B, 11), pr["c_y"], atol=1e-4)
     nat.close()
+
+
+def test_handle_info(native, monkeypatch):
+    """mpcmmd_handle_info reports the handle's implementation choices: the
+    beta-CEM generator variant follows the handle's capacity (<= 512
+    candidates and n <= 24: one wave per block), so the same problem can carry
+    different bits on handles of 512 and 1024 candidates; MPCMMD_GENWAVE pins
+    it."""
+    def info(B, **env):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        h = native.Handle(native.make_config(22, 10, 0.1, 30, "gaussian", 0.0, 0.0, num_batch=B, maxiter_cem=2))
+        out = {k: h.info(k) for k in ("gen_wave", "select_prep", "fused_small", "groups", "capacity")}
+        h.close()
+        for k in env:
+            monkeypatch.delenv(k)
+        return out
+    a, b = info(512), info(1024)
+    assert (a["gen_wave"], b["gen_wave"]) == (1, 0)
+    assert (a["capacity"], b["capacity"]) == (512, 1024)
+    assert b["groups"] == 2 and a["select_prep"] == 1
+    assert info(512, MPCMMD_GENWAVE="0")["gen_wave"] == 0
+    assert info(1024, MPCMMD_SELECT_PREP="0")["select_prep"] == 0
+    h = native.Handle(native.make_config(8, 3, 0.1, 10, "gaussian", 0.0, 0.0, num_batch=32, maxiter_cem=2))
+    with pytest.raises(native.NativeError, match="unknown handle_info"):
+        h.info("nonsense")
+    h.close()

@@ -15,7 +15,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 G = os.path.join(ROOT, "gpurun_out")
-P = os.path.join(ROOT, "profiles")
+# PROFILES_OUT: write elsewhere (the GPU box: gpurun_out/profiles_TAG, so only
+# the summaries travel back)
+P = os.environ.get("PROFILES_OUT", os.path.join(ROOT, "profiles"))
 
 
 def run(*a):
@@ -25,8 +27,10 @@ def run(*a):
 def main():
     tag = sys.argv[1]
     out = lambda name: os.path.join(P, f"{tag}_{name}")  # noqa: E731
+    os.makedirs(P, exist_ok=True)
     shutil.copy(os.path.join(G, f"bench_default_{tag}.json"), out("bench_default.json"))
-    shutil.copy(os.path.join(G, "gpu_tests.log"), out("gpu_tests.log"))
+    if os.path.exists(os.path.join(G, "gpu_tests.log")):
+        shutil.copy(os.path.join(G, "gpu_tests.log"), out("gpu_tests.log"))
     traffic = {}
     for wl, d in (("mmdopt", f"prof_{tag}"), ("cvar", f"prof_{tag}_cvar")):
         src = os.path.join(G, d)
