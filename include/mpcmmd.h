@@ -290,7 +290,11 @@ int mpcmmd_write(mpcmmd_handle* h, const char* name, const void* src, size_t byt
  *   2 risk       noisy rollouts + collision residual + risk reducer per candidate
  *                (cem_helper.py:402-538, costs.py:50-234, compute_beta.py:93-157)
  *   3 select     argsorts, compute_cost, elites, compute_shifted_samples
- *                (cem.py:233-315, cem_helper.py:232-314)
+ *                (cem.py:233-315, cem_helper.py:232-314).  With the select
+ *                preparation on (mpcmmd_handle_info "select_prep": cvar / saa /
+ *                mmd_random) stage 2 sorts the residuals and forms the cost
+ *                norms, so stage 3 needs stage 2 of the same iteration after
+ *                stage 1 (else MPCMMD_E_INVALID)
  * cost = mmd_opt splits stage 2 into sub-stages (t = outer iteration for 4, 8;
  * t = beta-CEM iteration 0..19 for 5-7):
  *   4 mother     noisy rows, n^2 mother rollouts, Bernstein fit (cem_helper.py:469-564)
