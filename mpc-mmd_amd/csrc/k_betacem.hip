@@ -226,9 +226,18 @@ __global__ __launch_bounds__(kDistThreads) void k_bdist(Params p) {
           const int r = 4 * rg + rr;
           if (r < rn) {
             const float* fr = Fr[r];  // wave-uniform: LDS broadcast
-            float d = fabsf(fr[0] - fj[0]);
+            // the differences two features at a time (v_pk_add_f32: the same
+            // roundings as two v_sub_f32), the sum sequential as before
+            static_assert(kF % 2 == 0, "feature pairs");
+            f2 df = f2{fr[0], fr[1]} - f2{fj[0], fj[1]};
+            float d = fabsf(df.x);
+            d = d + fabsf(df.y);
 #pragma unroll
-            for (int f = 1; f < kF; ++f) d = d + fabsf(fr[f] - fj[f]);
+            for (int f = 2; f < kF; f += 2) {
+              df = f2{fr[f], fr[f + 1]} - f2{fj[f], fj[f + 1]};
+              d = d + fabsf(df.x);
+              d = d + fabsf(df.y);
+            }
             D[size_t(r) * Md + j] = j < M ? d : __builtin_inff();
             dv[rr] = d;
           }
@@ -437,6 +446,172 @@ __global__ __launch_bounds__(64 * kMomRowsPerBlock) void k_bmoment(Params p) {
       for (int t = 0; t < NV4; ++t) x[t] = xn[t];
     }
   }
+}
+#endif
+
+// k_bmoment_rows: the same series records (and first-iteration direct sums)
+// with a distance row on one 16-lane DPP row instead of a whole wave: four
+// rows per wave, NV float4s (4 NV columns) per lane.  The per-row work that
+// does not scale with the row length -- the maximum, the division, the
+// totals of the eleven moments, the record store -- is then shared by four
+// times the columns per lane: 16-lane reductions (two quad_perm and two
+// row_ror DPP steps) instead of 64-lane ones, and the eleven totals by one
+// transposing butterfly over the row (row_mirror, row_half_mirror and the
+// two quad pairings: lane l ends with slot l of the record).  Same values as
+// bmoment_row up to the summation order of the moments and direct sums.
+// Columns j = 4 (l + 16 t) + c, l = lane & 15.
+DEVI float row16_max(float v) {
+  v = fmaxf(v, dpp_keep_f<0xB1>(v));
+  v = fmaxf(v, dpp_keep_f<0x4E>(v));
+  v = fmaxf(v, dpp_keep_f<0x124>(v));
+  return fmaxf(v, dpp_keep_f<0x128>(v));
+}
+DEVI float row16_total(float v) {
+  v += __int_as_float(dpp_i<0xB1>(__float_as_int(v)));
+  v += __int_as_float(dpp_i<0x4E>(__float_as_int(v)));
+  v += __int_as_float(dpp_i<0x124>(__float_as_int(v)));
+  return v + __int_as_float(dpp_i<0x128>(__float_as_int(v)));
+}
+// 16 per-lane values -> lane l (of each 16-lane row) holds the row total of v[l & 15]
+DEVI float row16_totals16(const float (&v)[16]) {
+  const int lane = tidx() & 15;
+  const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2, b0 = lane & 1;
+  float y[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {  // row_mirror: l <-> 15 - l (bit 3 flipped)
+    const float keep = b3 ? v[i + 8] : v[i], send = b3 ? v[i] : v[i + 8];
+    y[i] = keep + __int_as_float(dpp_i<0x140>(__float_as_int(send)));
+  }
+  float z[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // row_half_mirror: l <-> l ^ 7 (bit 2 flipped)
+    const float keep = b2 ? y[i + 4] : y[i], send = b2 ? y[i] : y[i + 4];
+    z[i] = keep + __int_as_float(dpp_i<0x141>(__float_as_int(send)));
+  }
+  float w[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // quad_perm(2,3,0,1): l <-> l ^ 2
+    const float keep = b1 ? z[i + 2] : z[i], send = b1 ? z[i] : z[i + 2];
+    w[i] = keep + __int_as_float(dpp_i<0x4E>(__float_as_int(send)));
+  }
+  const float keep = b0 ? w[1] : w[0], send = b0 ? w[0] : w[1];  // quad_perm(1,0,3,2): l <-> l ^ 1
+  return keep + __int_as_float(dpp_i<0xB1>(__float_as_int(send)));
+}
+
+template <int NV>
+DEVI void bmoment_row16(const Params& p, int g, bool live, const float4 (&x)[NV], int q0, int q1) {
+  const int l = tidx() & 15, grp = (tidx() & 63) >> 4;
+  const int M = p.M;
+  const int b = g / M;
+  // M > dist_stride(M) - 256, so the columns of t < NV - 4 are all real; only
+  // the last four float4s of a lane can hold pad columns (+inf)
+  auto sure = [](int t) { return t < NV - 4; };
+  auto valid = [&](int t, int c) { return sure(t) || 4 * (l + 16 * t) + c < M; };
+  // the row maximum on the bit patterns: distances are >= +0 (sums of fabsf),
+  // where unsigned order is float order (and no canonicalising v_max per
+  // element).  A NaN distance (NaN features) now makes R NaN where fmaxf
+  // skipped it; its row's sums are NaN either way (t = NaN for that column)
+  auto key = [](float v) { return __float_as_uint(v); };
+  uint32_t mb = 0u;
+#pragma unroll
+  for (int t = 0; t < NV; ++t) {
+    const float e[4] = {x[t].x, x[t].y, x[t].z, x[t].w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) mb = max(mb, valid(t, c) ? key(e[c]) : 0u);
+  }
+  const float R = 0.5f * row16_max(__uint_as_float(mb));
+  const float invR = R > 0.0f ? 1.0f / R : 0.0f;  // R = 0: every t = -1, every a = 0
+  f2 acc[kMom - 1];
+#pragma unroll
+  for (int k = 0; k < kMom - 1; ++k) acc[k] = f2{0.0f, 0.0f};
+#pragma unroll
+  for (int t = 0; t < NV; ++t) {
+    const float e[4] = {x[t].x, x[t].y, x[t].z, x[t].w};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float t0 = valid(t, 2 * h) ? fmaf(e[2 * h], invR, -1.0f) : 0.0f;
+      const float t1 = valid(t, 2 * h + 1) ? fmaf(e[2 * h + 1], invR, -1.0f) : 0.0f;
+      const f2 tt = {t0, t1};
+      f2 pw = tt;
+#pragma unroll
+      for (int k = 0; k < kMom - 1; ++k) {
+        acc[k] += pw;
+        if (k + 1 < kMom - 1) pw *= tt;
+      }
+      // one column pair's powers at a time (left to itself the scheduler
+      // interleaves all of them: 230 VGPRs)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  float v[16];  // slot k + 1 of the record: P_{k+1}
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = k >= 1 && k < kMom ? acc[k - 1].x + acc[k - 1].y : 0.0f;
+  float rec = row16_totals16(v);
+  if (l == 0) rec = float(M);
+  if (l == kMomR) rec = R;
+  if (live) p.bmom[size_t(g) * kMomStride + l] = rec;
+  // first-iteration pairs of this row that the series does not cover (k_bkernel's
+  // test, on the same R and sigma; rare: none at the BASELINE shapes), each
+  // 16-lane row on its own records, the wave looping while any row has one
+  // left (a whole wave per pair would need the rows in LDS: 48 KB per
+  // workgroup, three instead of four workgroups per CU for the record pass)
+  const int n = p.n;
+  float* rowsum = p.brow + size_t(b) * kBetaSamples * n;
+  int nmax = q1 - q0;
+  nmax = max(nmax, __shfl_xor(nmax, 16));
+  nmax = max(nmax, __shfl_xor(nmax, 32));
+  for (int c0 = 0; c0 < nmax; c0 += 16) {  // wave-uniform
+    const int c = q0 + c0 + l;
+    const bool have = c < q1;
+    const int2 pr = p.rpair0[have ? c : max(q0, 0)];
+    const int il = pr.x;
+    const float sl = __int_as_float(pr.y);
+    bool todo = have && !(double(R) * (1.0 / double(sl)) <= kSeriesAMaxRow);
+    while (__ballot(todo)) {  // wave-uniform
+      const unsigned field = unsigned(__ballot(todo) >> (16 * grp)) & 0xFFFFu;
+      const int j = field ? __builtin_ctz(field) : 0;
+      const int src = 16 * grp + j;
+      const int i = __shfl(il, src);
+      const float sg = __int_as_float(__shfl(__float_as_int(sl), src));
+      const float cs = kNegLog2eRow / sg;
+      const f2 c2 = {cs, cs};
+      f2 acc2 = {0.0f, 0.0f};
+#pragma unroll
+      for (int t = 0; t < NV; ++t) {  // pad columns: +inf * cs = -inf -> 0
+        const f2 t0 = f2{x[t].x, x[t].y} * c2, t1 = f2{x[t].z, x[t].w} * c2;
+        acc2 += f2{__builtin_amdgcn_exp2f(t0.x), __builtin_amdgcn_exp2f(t0.y)};
+        acc2 += f2{__builtin_amdgcn_exp2f(t1.x), __builtin_amdgcn_exp2f(t1.y)};
+      }
+      const float sum = row16_total(acc2.x + acc2.y);
+      if (field && l == 0) rowsum[i] = sum;
+      if (field && l == j) todo = false;
+    }
+  }
+}
+
+constexpr int kMomRowWaves = 4;  // waves per k_bmoment_rows workgroup
+
+#ifndef MPCMMD_FUSED_TU
+// four rows per wave and nothing else: measured against 2-16 four-row passes
+// per wave with the next pass's rows in flight (0.306 vs 0.318-0.363 ms per
+// configs[1] step), more resident waves hide the row loads better than a
+// prefetch within each
+template <int NV>
+__global__ __launch_bounds__(64 * kMomRowWaves) void k_bmoment_rows(Params p) {
+  const int l = tidx() & 15;
+  const int total = p.Bt * p.M, Md = dist_stride(p.M), M = p.M;
+  const int w = blockIdx.x * kMomRowWaves + (tidx() >> 6);
+  if (w * 4 >= total) return;  // wave-uniform
+  const int g = w * 4 + ((tidx() & 63) >> 4);
+  // rows past the end (the last wave's) compute on a clamped row, store nothing
+  const bool live = g < total;
+  const int gc = live ? g : total - 1;
+  const float4* row = reinterpret_cast<const float4*>(p.bdist + size_t(gc) * Md) + l;
+  float4 x[NV];
+#pragma unroll
+  for (int t = 0; t < NV; ++t) x[t] = row[16 * t];
+  const int q0 = live ? p.rp0[gc % M] : 0, q1 = live ? p.rp0[gc % M + 1] : 0;
+  bmoment_row16<NV>(p, gc, live, x, q0, q1);
 }
 #endif
 
@@ -3225,7 +3400,27 @@ void launch_bmoment_v(const Params& p, hipStream_t s) {
                      dim3(64 * kMomRowsPerBlock), 0, s, p);
 }
 
+template <int NV>
+void launch_bmoment_rows(const Params& p, hipStream_t s) {
+  const size_t rows = size_t(p.Bt) * p.M, per = size_t(kMomRowWaves) * 4;
+  hipLaunchKernelGGL((k_bmoment_rows<NV>), dim3((rows + per - 1) / per), dim3(64 * kMomRowWaves), 0, s, p);
+}
+
 void launch_bmoment(const Params& p, hipStream_t s) {
+  if (p.mom_rows) {
+    switch (dist_stride(p.M) >> 8) {  // 16 lanes x NV float4s = one row of dist_stride(M) columns
+      case 1:
+        return launch_bmoment_rows<4>(p, s);
+      case 2:
+        return launch_bmoment_rows<8>(p, s);
+      case 3:
+        return launch_bmoment_rows<12>(p, s);
+      case 4:
+        return launch_bmoment_rows<16>(p, s);
+      default:
+        break;
+    }
+  }
   switch (dist_stride(p.M) >> 8) {
 #define MPCMMD_MOM_CASE(V) \
   case V:                  \

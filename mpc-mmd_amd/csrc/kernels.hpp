@@ -109,6 +109,8 @@ struct Params {
   int32_t dir_waves;       // waves per k_bdirect workgroup (4, 8 or 16)
   int32_t ker_target;      // k_bkernel parts: enough for this many workgroups per launch (default 512)
   int32_t dir_target;      // k_bdirect parts: enough for this many workgroups per launch (default 2048)
+  int32_t mom_rows;        // 1 (default): k_bmoment_rows (16 lanes per distance row, 4 rows per wave); 0: a wave
+                           // per row (MPCMMD_MOM_ROWS=0)
   int32_t gen_wave;        // 1: beta-CEM generators by k_bgen_wave (a wave per block: the latency-bound small
                            // batches, Bt <= 512); 0: k_bgen (a quad per block: throughput). Fixed per handle.
   const float* beta_z0;    // [100][M+1]

@@ -748,6 +748,8 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     // the batch is split into groups or whether k_bcem_small runs it
     p.gen_wave = BT <= 512 && h->n <= 24;
     if (const char* g = std::getenv("MPCMMD_GENWAVE")) p.gen_wave = std::atoi(g) != 0;
+    p.mom_rows = 1;
+    if (const char* g = std::getenv("MPCMMD_MOM_ROWS")) p.mom_rows = std::atoi(g) != 0;
     p.dir_pairs = 1;
     if (const char* g = std::getenv("MPCMMD_DIR_PAIRS")) p.dir_pairs = std::atoi(g) != 0;
     p.qp_small = 1;
