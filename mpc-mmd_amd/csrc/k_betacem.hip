@@ -386,7 +386,7 @@ DEVI void bmoment_row(const Params& p, int gw, const float4 (&x)[NV4], const Row
     const int2 pr = c0 == q0 ? rq.pr : p.rpair0[min(c0 + lane, q1 - 1)];
     const int il = pr.x;
     const float sl = __int_as_float(pr.y);
-    const bool dl = !(double(R) * (1.0 / double(sl)) <= kSeriesAMaxRow) && c0 + lane < q1;
+    const bool dl = !(double(R) * (1.0 / double(sl)) <= p.mom_amax) && c0 + lane < q1;
     unsigned long long todo = __ballot(dl);
     while (todo) {  // wave-uniform
       const int j = __builtin_ctzll(todo);
@@ -566,7 +566,7 @@ DEVI void bmoment_row16(const Params& p, int g, bool live, const float4 (&x)[NV]
     const int2 pr = p.rpair0[have ? c : max(q0, 0)];
     const int il = pr.x;
     const float sl = __int_as_float(pr.y);
-    bool todo = have && !(double(R) * (1.0 / double(sl)) <= kSeriesAMaxRow);
+    bool todo = have && !(double(R) * (1.0 / double(sl)) <= p.mom_amax);
     while (__ballot(todo)) {  // wave-uniform
       const unsigned field = unsigned(__ballot(todo) >> (16 * grp)) & 0xFFFFu;
       const int j = field ? __builtin_ctz(field) : 0;
@@ -602,15 +602,17 @@ __global__ __launch_bounds__(64 * kMomRowWaves) void k_bmoment_rows(Params p) {
   const int total = p.Bt * p.M, Md = dist_stride(p.M), M = p.M;
   const int w = blockIdx.x * kMomRowWaves + (tidx() >> 6);
   if (w * 4 >= total) return;  // wave-uniform
-  const int g = w * 4 + ((tidx() & 63) >> 4);
-  // rows past the end (the last wave's) compute on a clamped row, store nothing
-  const bool live = g < total;
-  const int gc = live ? g : total - 1;
+  // position gp of the candidates' rows in pair-count order (Params::rperm): the
+  // wave's four rows carry nearly the same number of first-iteration pairs
+  const int gp = w * 4 + ((tidx() & 63) >> 4);
+  // positions past the end (the last wave's) compute on a clamped row, store nothing
+  const bool live = gp < total;
+  const int gpc = live ? gp : total - 1, bc = gpc / M, r = p.rperm[gpc - bc * M], gc = bc * M + r;
   const float4* row = reinterpret_cast<const float4*>(p.bdist + size_t(gc) * Md) + l;
   float4 x[NV];
 #pragma unroll
   for (int t = 0; t < NV; ++t) x[t] = row[16 * t];
-  const int q0 = live ? p.rp0[gc % M] : 0, q1 = live ? p.rp0[gc % M + 1] : 0;
+  const int q0 = live ? p.rp0[r] : 0, q1 = live ? p.rp0[r + 1] : 0;
   bmoment_row16<NV>(p, gc, live, x, q0, q1);
 }
 #endif

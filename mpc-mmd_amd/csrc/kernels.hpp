@@ -111,6 +111,8 @@ struct Params {
   int32_t dir_target;      // k_bdirect parts: enough for this many workgroups per launch (default 2048)
   int32_t mom_rows;        // 1 (default): k_bmoment_rows (16 lanes per distance row, 4 rows per wave); 0: a wave
                            // per row (MPCMMD_MOM_ROWS=0)
+  double mom_amax;         // k_bmoment's first-iteration direct test a > mom_amax: kSeriesAMax (1.0), k_bkernel's;
+                           // MPCMMD_MOM_AMAX (tests only: 0 sends every first-iteration pair to the direct sums)
   int32_t gen_wave;        // 1: beta-CEM generators by k_bgen_wave (a wave per block: the latency-bound small
                            // batches, Bt <= 512); 0: k_bgen (a quad per block: throughput). Fixed per handle.
   const float* beta_z0;    // [100][M+1]
@@ -149,6 +151,8 @@ struct Params {
   const float* sig0;       // [100]        its sigma
   const int32_t* rp0;      // [M+1]        pairs of mother row r: rpair0[rp0[r] .. rp0[r+1])
   const int2* rpair0;      // [100 n]      pair (i = s n + k, sigma_s bits), grouped by row
+  const int32_t* rperm;    // [M]          mother rows by descending pair count (k_bmoment_rows: four rows of
+                           //              nearly equal count per wave, so its direct-sum loop idles little)
   int32_t* bdcount;        // [B][kMaxSplit] their count per k_bkernel part
   float* bdist;            // [B][M][dist_stride(M)] L1 distances of the mother features
                            //              (kernel_computation.py:33-39), once per outer iteration

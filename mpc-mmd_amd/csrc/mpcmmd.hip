@@ -320,6 +320,10 @@ void ensure_sel0(mpcmmd_handle* h) {
   upload(h, "sig0", sig.data(), kBetaSamples * 4);
   upload(h, "rp0", rp.data(), (M + 1) * 4);
   upload(h, "rpair0", pairs.data(), size_t(np) * 8);
+  std::vector<int32_t> perm(M);
+  for (int r = 0; r < M; ++r) perm[r] = r;
+  std::stable_sort(perm.begin(), perm.end(), [&](int a, int c) { return rp[a + 1] - rp[a] > rp[c + 1] - rp[c]; });
+  upload(h, "rperm", perm.data(), size_t(M) * 4);
   HIPC(hipStreamSynchronize(h->stream));  // host temporaries
   h->sel0_valid = true;
   ++h->sel0_gen;
@@ -663,6 +667,7 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
       p.sig0 = (const float*)h->alloc("sig0", size_t(kBetaSamples) * 4);
       p.rp0 = (const int32_t*)h->alloc("rp0", (M + 1) * 4);
       p.rpair0 = (const int2*)h->alloc("rpair0", size_t(kBetaSamples) * n * 8);
+      p.rperm = (const int32_t*)h->alloc("rperm", size_t(M) * 4);
       p.bdist = (float*)h->alloc("bdist", BT * M * dist_stride(int(M)) * 4);
       p.ctrl_n = (float*)h->alloc("ctrl_n", BT * 2 * n * H * 4);
       p.bsel = (int32_t*)h->alloc("bsel", BT * kBetaSamples * n * 4);
@@ -750,6 +755,8 @@ int mpcmmd_create_batch(const mpcmmd_config* cfg, int32_t max_configs, mpcmmd_ha
     if (const char* g = std::getenv("MPCMMD_GENWAVE")) p.gen_wave = std::atoi(g) != 0;
     p.mom_rows = 1;
     if (const char* g = std::getenv("MPCMMD_MOM_ROWS")) p.mom_rows = std::atoi(g) != 0;
+    p.mom_amax = 1.0;  // == kSeriesAMax
+    if (const char* g = std::getenv("MPCMMD_MOM_AMAX")) p.mom_amax = std::atof(g);
     p.dir_pairs = 1;
     if (const char* g = std::getenv("MPCMMD_DIR_PAIRS")) p.dir_pairs = std::atoi(g) != 0;
     p.qp_small = 1;

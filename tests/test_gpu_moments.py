@@ -9,6 +9,8 @@ row maximum R, the record's M slot and the set of direct pairs are exact."""
 import numpy as np
 import pytest
 
+import oracle
+
 from parity import DEFAULT_COV, DEFAULT_INIT, DEFAULT_MEAN, make_pair
 
 pytestmark = pytest.mark.gpu
@@ -16,10 +18,12 @@ pytestmark = pytest.mark.gpu
 F32, F64 = np.float32, np.float64
 
 
-def _moments(native, monkeypatch, rows, n, B, H, O):
+def _moments(native, monkeypatch, rows, n, B, H, O, level=None):
     monkeypatch.setenv("MPCMMD_MOM_ROWS", rows)
-    ora, nat, xo, yo = make_pair(native, "mmd_opt", n=n, O=O, H=H, B=B, T=2)
-    nat.begin("mmd_opt", 7, DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, xo, yo, 15.0)
+    ora, nat, xo, yo = make_pair(native, "mmd_opt", n=n, O=O, H=H, B=B, T=2, level=level)
+    # explicit noise tables (the mother rows' noise), as test_gpu_parity_mmdopt
+    draws = oracle.Draws.random(ora.prob, np.random.default_rng(1), idx_mpc=11, seed=0, with_beta_cem=True)
+    nat.begin("mmd_opt", 11, DEFAULT_INIT, DEFAULT_MEAN, DEFAULT_COV, xo, yo, 15.0, draws)
     nat.run_stage(1, 0)
     nat.sync()
     brow0 = np.full(nat.read("brow").shape, np.nan, F32)
@@ -31,14 +35,16 @@ def _moments(native, monkeypatch, rows, n, B, H, O):
     return out
 
 
-@pytest.mark.parametrize("n,B,H,O", [(6, 24, 12, 3), (10, 20, 30, 4), (22, 21, 30, 10), (32, 20, 20, 4)])
-def test_moment_rows(native, monkeypatch, n, B, H, O):
+@pytest.mark.parametrize("n,B,H,O,level", [(6, 24, 12, 3, None), (10, 20, 30, 4, None), (22, 21, 30, 10, None),
+                                           (32, 20, 20, 4, None), (22, 20, 30, 4, 30.0)])
+def test_moment_rows(native, monkeypatch, n, B, H, O, level):
     M = n * n
     Md = (M + 255) & ~255
-    old = _moments(native, monkeypatch, "0", n, B, H, O)
-    new = _moments(native, monkeypatch, "1", n, B, H, O)
+    old = _moments(native, monkeypatch, "0", n, B, H, O, level)
+    new = _moments(native, monkeypatch, "1", n, B, H, O, level)
     assert np.array_equal(old["bdist"], new["bdist"])
     D = new["bdist"].reshape(B * M, Md)[:, :M].astype(F64)
+    assert D.max() > 0 and (D == 0).mean() < 1.0 / M + 0.01, "degenerate mother rows"  # zeros: the diagonal
     ro = old["bmom"].reshape(B * M, 16)
     rn = new["bmom"].reshape(B * M, 16)
     # exact: the M slot, R (a maximum) and the unused slots
@@ -64,3 +70,20 @@ def test_moment_rows(native, monkeypatch, n, B, H, O):
         a, b = new["brow"][wn].astype(F64), old["brow"][wo].astype(F64)
         assert np.all(np.abs(a - b) <= 2e-5 * np.abs(b)), "direct sums"
     print(f"n={n}: {int((~np.isnan(new['brow'])).sum())} direct first-iteration sums")
+
+
+@pytest.mark.parametrize("n,B", [(10, 20), (22, 21)])
+def test_moment_rows_direct_sums(native, monkeypatch, n, B):
+    """Every first-iteration pair sent to the direct sums (MPCMMD_MOM_AMAX=0:
+    the direct test is a > 0; at the BASELINE shapes a <= 1 for nearly every
+    pair, so the default tests write none): both kernels write the same pairs,
+    each sum_j exp(-D[r][j] / sigma) to fp32 rounding of NumPy's."""
+    monkeypatch.setenv("MPCMMD_MOM_AMAX", "0")
+    H, O, M = 30, 4, n * n
+    Md = (M + 255) & ~255
+    old = _moments(native, monkeypatch, "0", n, B, H, O)
+    new = _moments(native, monkeypatch, "1", n, B, H, O)
+    wo, wn = ~np.isnan(old["brow"]), ~np.isnan(new["brow"])
+    assert np.array_equal(wo, wn) and wn.all(), "every (sample, row) pair written by both"
+    a, b = new["brow"].astype(F64), old["brow"].astype(F64)
+    assert np.all(np.abs(a - b) <= 2e-5 * np.abs(b)), "direct sums"
