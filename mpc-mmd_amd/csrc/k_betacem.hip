@@ -104,7 +104,14 @@ DEVI float kred_perturb(float v, int e) {
 // ------------------------------------------------------------------------
 // k_mother
 #ifndef MPCMMD_FUSED_TU
-__global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
+// CARLA (the fp64 tan / per-row initial states) and the static rollouts as two
+// instantiations: the static one's registers no longer carry the CARLA path
+// (166 -> fewer VGPRs, SGPR spills gone: two 512-thread workgroups per CU)
+#ifndef MPCMMD_MOTHER_WAVES
+#define MPCMMD_MOTHER_WAVES 1
+#endif
+template <bool CARLA>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(CARLA ? 1 : MPCMMD_MOTHER_WAVES))) void k_mother(Params p, int t) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = p.n, H = p.H, M = p.M, b = blockIdx.x;
   const Cfg cf = cfg_of(p, b / p.B);
@@ -118,7 +125,7 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
     noisy_control(p, cf, t, r, h, p.acc[size_t(b) * 100 + h], p.steer[size_t(b) * 100 + h], a, s);
     an[idx] = a;
     sn[idx] = s;
-    if (p.carla) tn[idx] = float(tan(double(s)));
+    if constexpr (CARLA) tn[idx] = float(tan(double(s)));
     gctrl[idx] = a;
     gctrl[n * H + idx] = s;
   }
@@ -131,7 +138,7 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
     const float* tr = tn + (m % n) * H;
     // CARLA: every mother row starts from its own noisy initial state
     // (carla/optimizer/cem.py:251-253, cem_helper.py:846)
-    const float* st = p.carla ? p.st0r + (size_t(cf.g) * p.R0 + m) * 8 : cf.st0;
+    const float* st = CARLA ? p.st0r + (size_t(cf.g) * p.R0 + m) * 8 : cf.st0;
     float x = st[0], y = st[1], vx = st[2], vy = st[3], psi = st[4];
     double cx[11], cy[11];
 #pragma unroll
@@ -145,7 +152,7 @@ __global__ __launch_bounds__(kThreads) void k_mother(Params p, int t) {
         cy[k] = cy[k] + f * dy;
       }
       if (h == H - 1) break;
-      if (p.carla) bicycle_step_cr_t(x, y, vx, vy, psi, ar[h], tr[h], p.wheel_base);
+      if constexpr (CARLA) bicycle_step_cr_t(x, y, vx, vy, psi, ar[h], tr[h], p.wheel_base);
       else bicycle_step(x, y, vx, vy, psi, ar[h], sr[h]);
     }
     float fr[kFeatStride];
@@ -3387,7 +3394,10 @@ bool mmdopt_supported(int n, int H, int O, std::string* why) {
 }
 
 void launch_mother(const Params& p, int t, hipStream_t s) {
-  hipLaunchKernelGGL(k_mother, dim3(p.Bt), dim3(kThreads), size_t(3) * p.n * p.H * 4, s, p, t);
+  if (p.carla)
+    hipLaunchKernelGGL(k_mother<true>, dim3(p.Bt), dim3(kThreads), size_t(3) * p.n * p.H * 4, s, p, t);
+  else
+    hipLaunchKernelGGL(k_mother<false>, dim3(p.Bt), dim3(kThreads), size_t(3) * p.n * p.H * 4, s, p, t);
 }
 
 void launch_bdist(const Params& p, hipStream_t s) {
