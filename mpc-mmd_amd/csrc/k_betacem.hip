@@ -558,10 +558,10 @@ DEVI void bmoment_row16(const Params& p, int g, bool live, const float4 (&x)[NV]
   if (l == kMomR) rec = R;
   if (live) p.bmom[size_t(g) * kMomStride + l] = rec;
   // first-iteration pairs of this row that the series does not cover (k_bkernel's
-  // test, on the same R and sigma; rare: none at the BASELINE shapes), each
-  // 16-lane row on its own records, the wave looping while any row has one
-  // left (a whole wave per pair would need the rows in LDS: 48 KB per
-  // workgroup, three instead of four workgroups per CU for the record pass)
+  // test, on the same R and sigma: about 3/4 of the pairs on real distances),
+  // each 16-lane row on its own records, one distinct sigma per round, the
+  // wave looping while any row has one left (a whole wave per pair would need
+  // the rows in LDS: 32-64 KB per workgroup, measured slower)
   const int n = p.n;
   float* rowsum = p.brow + size_t(b) * kBetaSamples * n;
   int nmax = q1 - q0;
@@ -578,7 +578,6 @@ DEVI void bmoment_row16(const Params& p, int g, bool live, const float4 (&x)[NV]
       const unsigned field = unsigned(__ballot(todo) >> (16 * grp)) & 0xFFFFu;
       const int j = field ? __builtin_ctz(field) : 0;
       const int src = 16 * grp + j;
-      const int i = __shfl(il, src);
       const float sg = __int_as_float(__shfl(__float_as_int(sl), src));
       const float cs = kNegLog2eRow / sg;
       const f2 c2 = {cs, cs};
@@ -590,8 +589,11 @@ DEVI void bmoment_row16(const Params& p, int g, bool live, const float4 (&x)[NV]
         acc2 += f2{__builtin_amdgcn_exp2f(t1.x), __builtin_amdgcn_exp2f(t1.y)};
       }
       const float sum = row16_total(acc2.x + acc2.y);
-      if (field && l == 0) rowsum[i] = sum;
-      if (field && l == j) todo = false;
+      // every pair of the row with this sigma (the first iteration's samples
+      // share sigma = 0.01, the clip, about half of them) takes the same sum
+      const bool same = todo && __float_as_uint(sl) == __float_as_uint(sg);
+      if (field && same) rowsum[il] = sum;
+      if (field && same) todo = false;
     }
   }
 }

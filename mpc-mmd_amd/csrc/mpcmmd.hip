@@ -320,9 +320,18 @@ void ensure_sel0(mpcmmd_handle* h) {
   upload(h, "sig0", sig.data(), kBetaSamples * 4);
   upload(h, "rp0", rp.data(), (M + 1) * 4);
   upload(h, "rpair0", pairs.data(), size_t(np) * 8);
-  std::vector<int32_t> perm(M);
-  for (int r = 0; r < M; ++r) perm[r] = r;
-  std::stable_sort(perm.begin(), perm.end(), [&](int a, int c) { return rp[a + 1] - rp[a] > rp[c + 1] - rp[c]; });
+  // k_bmoment_rows' row order: descending number of distinct sigmas among a
+  // row's pairs (its direct-sum rounds), so a wave's four rows need about the
+  // same number
+  std::vector<int32_t> perm(M), nsig(M, 0);
+  for (int r = 0; r < M; ++r) {
+    perm[r] = r;
+    std::vector<int32_t> sg;
+    for (int q = rp[r]; q < rp[r + 1]; ++q) sg.push_back(pairs[2 * q + 1]);
+    std::sort(sg.begin(), sg.end());
+    nsig[r] = int(std::unique(sg.begin(), sg.end()) - sg.begin());
+  }
+  std::stable_sort(perm.begin(), perm.end(), [&](int a, int c) { return nsig[a] > nsig[c]; });
   upload(h, "rperm", perm.data(), size_t(M) * 4);
   HIPC(hipStreamSynchronize(h->stream));  // host temporaries
   h->sel0_valid = true;
