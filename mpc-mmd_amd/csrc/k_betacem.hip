@@ -180,7 +180,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(CARLA 
 // of 20 times.  Workgroup = (candidate, tile of kDistRows rows); a thread
 // owns one column (its 22 features in registers), the tile's row features
 // are LDS broadcasts; the feature sum is sequential (the oracle's order).
-// Pad columns M..Md-1 hold +inf so exp2(-inf) = 0 in the row sums.
+// Pad columns M..Md-1 hold +inf so exp2(-inf) = 0 in the row sums (written
+// once per handle by k_dist_pad).
 constexpr int kDistRows = 32;
 constexpr int kDistThreads = 256;
 
@@ -245,7 +246,7 @@ __global__ __launch_bounds__(kDistThreads) void k_bdist(Params p) {
               d = d + fabsf(df.x);
               d = d + fabsf(df.y);
             }
-            D[size_t(r) * Md + j] = j < M ? d : __builtin_inff();
+            if (j < M) D[size_t(r) * Md + j] = d;  // pad columns: +inf once per handle (k_dist_pad)
             dv[rr] = d;
           }
         }
@@ -3400,6 +3401,24 @@ void launch_mother(const Params& p, int t, hipStream_t s) {
     hipLaunchKernelGGL(k_mother<true>, dim3(p.Bt), dim3(kThreads), size_t(3) * p.n * p.H * 4, s, p, t);
   else
     hipLaunchKernelGGL(k_mother<false>, dim3(p.Bt), dim3(kThreads), size_t(3) * p.n * p.H * 4, s, p, t);
+}
+
+// the pad columns M..Md-1 of every distance row, +inf (exp(-inf) = 0 in the
+// row sums): once per handle, k_bdist writes the real columns only
+#ifndef MPCMMD_FUSED_TU
+__global__ __launch_bounds__(256) void k_dist_pad(Params p, int cap) {
+  const int M = p.M, Md = dist_stride(M), np = Md - M;
+  const size_t total = size_t(cap) * M * np;
+  for (size_t x = size_t(blockIdx.x) * 256 + tidx(); x < total; x += size_t(gridDim.x) * 256) {
+    const size_t row = x / np;
+    p.bdist[row * Md + M + (x - row * np)] = __builtin_inff();
+  }
+}
+#endif
+
+void launch_dist_pad(const Params& p, int cap, hipStream_t s) {
+  if (dist_stride(p.M) == p.M) return;
+  hipLaunchKernelGGL(k_dist_pad, dim3(2048), dim3(256), 0, s, p, cap);
 }
 
 void launch_bdist(const Params& p, hipStream_t s) {

@@ -281,6 +281,7 @@ void launch_gamma_tab(const Params& p, int t, hipStream_t s);
 void launch_beta_planes(const Params& p, int t, hipStream_t s);
 // mmd_opt risk, one launch each (mpcmmd.hip chains them)
 void launch_mother(const Params& p, int t, hipStream_t s);
+void launch_dist_pad(const Params& p, int cap, hipStream_t s);  // once per handle (cap candidates), before the first launch_bdist
 void launch_bdist(const Params& p, hipStream_t s);
 void launch_bmoment(const Params& p, hipStream_t s);  // after launch_bdist: series records of the distance rows
 void launch_bsample(const Params& p, int tb, hipStream_t s);

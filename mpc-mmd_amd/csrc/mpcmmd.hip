@@ -92,6 +92,7 @@ struct mpcmmd_handle {
   int last_t = -1;
   bool ext_roll = false, ext_res = false;
   bool beta_tables_internal = false;  // device beta tables hold the internal streams
+  bool dist_pad = false;              // the distance matrix's +inf pad columns written (k_dist_pad)
   bool sel0_valid = false;            // sel0 / sig0 / rp0 / rpair0 match the device beta_z0
   // generation of the sel0 table (bumped by every rebuild) and the one
   // k_bmoment last used for the first beta-iteration's direct row sums: the
@@ -441,6 +442,10 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
         if (!h->mmd_ok) throw std::invalid_argument("mmd_opt unsupported for this configuration: " + h->mmd_why);
         ensure_sel0(h);
         h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
+        if (!h->dist_pad) {
+          launch_dist_pad(p, h->Gmax * h->B, h->stream);  // the whole capacity: later solves may hold more candidates
+          h->dist_pad = true;
+        }
         h->launch(kKBDist, [&] { launch_bdist(p, h->stream); });
         h->launch(kKBMoment, [&] { launch_bmoment(p, h->stream); });
         h->bmoment_gen = h->sel0_gen;
@@ -479,6 +484,10 @@ void run_stage(mpcmmd_handle* h, int stage, int t) {
         ensure_gamma_tab(h, t);
         ensure_sel0(h);
         h->launch(kKMother, [&] { launch_mother(p, t, h->stream); });
+        if (!h->dist_pad) {
+          launch_dist_pad(p, h->Gmax * h->B, h->stream);  // the whole capacity: later solves may hold more candidates
+          h->dist_pad = true;
+        }
         h->launch(kKBDist, [&] { launch_bdist(p, h->stream); });
         h->launch(kKBMoment, [&] { launch_bmoment(p, h->stream); });
         h->bmoment_gen = h->sel0_gen;
