@@ -3135,25 +3135,35 @@ __global__ __launch_bounds__(kThreads) void k_bsigma(Params p, int tb) {
 // k_mmdfinal: x_red / y_red of the best reduced set (compute_beta.py:465),
 // compute_mmd_obs (costs.py:173-186) and compute_mmd_lane (costs.py:121-135).
 #ifndef MPCMMD_FUSED_TU
+// Two phases: the n reduced rollouts a lane each, their states kept in LDS,
+// then the n H O obstacle terms over all 64 lanes, a (row, step) pair per
+// lane, the row maxima by LDS atomics on the bit patterns (every compared
+// value is >= +0 after the max with the initial 0, where unsigned order is
+// float order; a maximum is order-free, so the bits are the sequential
+// loop's).  The sequential form held 22 of 64 lanes through H x O f_bar
+// evaluations and their obstacle loads (62 us per configs[1] step).
 __global__ __launch_bounds__(64) void k_mmdfinal(Params p, int t) {
   __shared__ float cb[kMaxReduced], lb[kMaxReduced], ub[kMaxReduced], bt[kMaxReduced];
+  __shared__ uint32_t cbits[kMaxReduced], cnan[kMaxReduced];
   __shared__ ReduceScratch rs;
+  extern __shared__ __attribute__((aligned(16))) float xy[];  // [2][n][H] rollout states, then [2][n][H] controls
   const int b = blockIdx.x, n = p.n, H = p.H, O = p.O, lane = tidx();
   const Cfg cf = cfg_of(p, b / p.B);
-  const float* ctrl = p.ctrl_n + size_t(b) * 2 * n * H;
+  // the candidate's noisy controls staged by all lanes (coalesced), so the
+  // rollouts' per-step reads are LDS reads, not a global load latency per step
+  float* ctrl = xy + 2 * n * H;
+  for (int i = lane; i < 2 * n * H; i += 64) ctrl[i] = p.ctrl_n[size_t(b) * 2 * n * H + i];
+  __syncthreads();
   if (lane < n) {
     const int m = p.bestsel[size_t(b) * n + lane];
     const float* ar = ctrl + (m / n) * H;
     const float* sr = ctrl + n * H + (m % n) * H;
     float x = cf.st0[0], y = cf.st0[1], vx = cf.st0[2], vy = cf.st0[3], psi = cf.st0[4];
-    float c = 0.0f, l = 0.0f, u = 0.0f;
+    float l = 0.0f, u = 0.0f;
     bool nan = false;
     for (int h = 0; h < H; ++h) {
-      for (int o = 0; o < O; ++o) {
-        const float f = f_bar(x, y, cf.obs[o * H + h], cf.obs[O * H + o * H + h]);
-        nan |= (f != f);
-        c = fmaxf(c, f);
-      }
+      xy[lane * H + h] = x;
+      xy[(n + lane) * H + h] = y;
       nan |= (y != y);
       l = fmaxf(l, -y + p.y_lb);
       u = fmaxf(u, y - p.y_ub);
@@ -3161,11 +3171,28 @@ __global__ __launch_bounds__(64) void k_mmdfinal(Params p, int t) {
       bicycle_step(x, y, vx, vy, psi, ar[h], sr[h]);
     }
     const float qnan = __int_as_float(0x7fc00000);
-    cb[lane] = nan ? qnan : c;
+    cbits[lane] = 0u;
+    cnan[lane] = nan ? 1u : 0u;
     lb[lane] = nan ? qnan : l;
     ub[lane] = nan ? qnan : u;
     bt[lane] = p.beta[size_t(b) * n + lane];
   }
+  __syncthreads();
+  for (int e = lane; e < n * H; e += 64) {
+    const int k = e / H, h = e - k * H;
+    const float x = xy[e], y = xy[n * H + e];
+    float c = 0.0f;
+    bool nan = false;
+    for (int o = 0; o < O; ++o) {
+      const float f = f_bar(x, y, cf.obs[o * H + h], cf.obs[O * H + o * H + h]);
+      nan |= (f != f);
+      c = fmaxf(c, f);
+    }
+    atomicMax(&cbits[k], __float_as_uint(c + 0.0f));  // -0 -> +0 (fmaxf may keep -0): unsigned order = float order
+    if (nan) atomicOr(&cnan[k], 1u);
+  }
+  __syncthreads();
+  if (lane < n) cb[lane] = cnan[lane] ? __int_as_float(0x7fc00000) : __uint_as_float(cbits[lane]);
   __syncthreads();
   const float sigma = p.sigma[b];
   const float obs = block_mmd(cb, bt, n, sigma, 1000.0f, rs);
@@ -3651,7 +3678,7 @@ void launch_bgen(const Params& p, int tb, hipStream_t s) {
 
 // (k_bcem_small's generators are bgen_wave's: handles with gen_wave only)
 void launch_mmdfinal(const Params& p, int t, hipStream_t s) {
-  hipLaunchKernelGGL(k_mmdfinal, dim3(p.Bt), dim3(64), 0, s, p, t);
+  hipLaunchKernelGGL(k_mmdfinal, dim3(p.Bt), dim3(64), size_t(4) * p.n * p.H * 4, s, p, t);
 }
 
 #else
