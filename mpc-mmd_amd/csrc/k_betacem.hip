@@ -118,6 +118,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(CARLA 
   float* an = reinterpret_cast<float*>(smem);
   float* sn = an + n * H;
   float* tn = sn + n * H;  // CARLA: float(tan(double(steer))) of each control, off the rows' step chains
+  // the Bernstein fit rows by step, [H][11] doubles: a step's eleven factors as
+  // LDS broadcasts, not a scalar-load latency inside every step of the chain
+  double* fitl = reinterpret_cast<double*>(smem + ((size_t(3) * n * H * 4 + 15) & ~size_t(15)));
+  for (int idx = tidx(); idx < 11 * H; idx += blockDim.x) {
+    const int h = idx / 11, k = idx - h * 11;
+    fitl[idx] = p.fit[k * H + h];
+  }
   float* gctrl = p.ctrl_n + size_t(b) * 2 * n * H;
   for (int idx = tidx(); idx < n * H; idx += blockDim.x) {
     const int r = idx / H, h = idx % H;
@@ -147,7 +154,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(CARLA 
       const double dx = double(x), dy = double(y);
 #pragma unroll
       for (int k = 0; k < 11; ++k) {
-        const double f = p.fit[k * H + h];
+        const double f = fitl[h * 11 + k];
         cx[k] = cx[k] + f * dx;
         cy[k] = cy[k] + f * dy;
       }
@@ -3424,10 +3431,11 @@ bool mmdopt_supported(int n, int H, int O, std::string* why) {
 }
 
 void launch_mother(const Params& p, int t, hipStream_t s) {
+  const size_t lds = ((size_t(3) * p.n * p.H * 4 + 15) & ~size_t(15)) + size_t(11) * p.H * 8;  // controls, fit rows
   if (p.carla)
-    hipLaunchKernelGGL(k_mother<true>, dim3(p.Bt), dim3(kThreads), size_t(3) * p.n * p.H * 4, s, p, t);
+    hipLaunchKernelGGL(k_mother<true>, dim3(p.Bt), dim3(kThreads), lds, s, p, t);
   else
-    hipLaunchKernelGGL(k_mother<false>, dim3(p.Bt), dim3(kThreads), size_t(3) * p.n * p.H * 4, s, p, t);
+    hipLaunchKernelGGL(k_mother<false>, dim3(p.Bt), dim3(kThreads), lds, s, p, t);
 }
 
 // the pad columns M..Md-1 of every distance row, +inf (exp(-inf) = 0 in the
