@@ -207,6 +207,14 @@ HDI uint32_t sort_key(float x) {
   return (u >> 31) ? ~u : (u | 0x80000000u);
 }
 
+// sort_key(fabsf(x)) in four VALU operations: |x| has no sign and no -0, so
+// the key is its bit pattern with bit 31 set, or ~0 for a NaN (pattern above
+// +inf's) -- the same value for every x
+DEVI uint32_t sort_key_abs(float x) {
+  const uint32_t u = __float_as_uint(x) & 0x7FFFFFFFu;
+  return u > 0x7F800000u ? 0xFFFFFFFFu : (u | 0x80000000u);
+}
+
 // ---- arithmetic --------------------------------------------------------------
 // x / d for a divisor known in advance, r = RN(1/d): one FMA correction of
 // RN(x r).  Bit-equal to IEEE division for every x when d = 2.5, and for

@@ -651,7 +651,7 @@ DEVI void load_keys(V val, int M, uint32_t* key) {
   for (int q = 0; q < NQ; ++q) {
     const int j = lane + 64 * q;
     const float v = val(min(j, M - 1));
-    key[q] = j < M ? sort_key(fabsf(v)) : 0u;  // real keys have bit 31 set
+    key[q] = j < M ? sort_key_abs(v) : 0u;  // real keys have bit 31 set
   }
 }
 
