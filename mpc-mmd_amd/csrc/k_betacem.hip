@@ -2861,15 +2861,25 @@ DEVI void bgen_quad(const Params& p, int b, int blk, bool live) {
   const int j0 = blk * 16, j1 = min(M1, j0 + 16);
   double un[11];  // the quad's four lanes load the same 88 bytes; the next
                   // position's u in flight while one is processed
+  double uon[3];  // and the lane's own components u[q + 4 i] (slot 11, the
+                  // mean, loaded and masked), so the dot u . v needs no
+                  // lane-dependent register selects
+  const double* ub = gen + gen_uplane(pos_pad(M));
 #pragma unroll
-  for (int c = 0; c < 11; ++c) un[c] = gen[gen_uplane(pos_pad(M)) + size_t(j0) * kGenRow + c];
+  for (int c = 0; c < 11; ++c) un[c] = ub[size_t(j0) * kGenRow + c];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) uon[i] = ub[size_t(j0) * kGenRow + q + 4 * i];
   for (int j = j0; j < j1; ++j) {
-    double u[11];
+    double u[11], uo[3];
 #pragma unroll
     for (int c = 0; c < 11; ++c) u[c] = un[c];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) uo[i] = uon[i];
     const int jn = min(j + 1, j1 - 1);
 #pragma unroll
-    for (int c = 0; c < 11; ++c) un[c] = gen[gen_uplane(pos_pad(M)) + size_t(jn) * kGenRow + c];
+    for (int c = 0; c < 11; ++c) un[c] = ub[size_t(jn) * kGenRow + c];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) uon[i] = ub[size_t(jn) * kGenRow + q + 4 * i];
     double v[3], part = 0.0;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -2878,7 +2888,7 @@ DEVI void bgen_quad(const Params& p, int b, int blk, bool live) {
       for (int c = 0; c < 11; ++c) s = fma(A[i][c], u[c], s);
       v[i] = s;
       const int a = q + 4 * i;
-      part = fma(a < 11 ? u[min(a, 10)] : 0.0, s, part);
+      part = fma(i < 2 || a < 11 ? uo[i] : 0.0, s, part);
     }
     const double uv = quad_sum(part);
     const double ljj = sqrt(kRidge + uv);
