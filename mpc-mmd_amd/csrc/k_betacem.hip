@@ -253,13 +253,20 @@ __global__ __launch_bounds__(kDistThreads) void k_bdist(Params p) {
               d = d + fabsf(df.x);
               d = d + fabsf(df.y);
             }
+#if defined(MPCMMD_BDIST_VARIANT) && MPCMMD_BDIST_VARIANT == 2
+            if (d == -1.0f) D[size_t(r) * Md + j] = d;  // timing build: no row stores
+#else
             if (j < M) D[size_t(r) * Md + j] = d;  // pad columns: +inf once per handle (k_dist_pad)
+#endif
             dv[rr] = d;
           }
         }
         *reinterpret_cast<float4*>(&Tm[tid * kMirrorPitch + 4 * rg]) = make_float4(dv[0], dv[1], dv[2], dv[3]);
       }
     }
+#if defined(MPCMMD_BDIST_VARIANT) && MPCMMD_BDIST_VARIANT >= 1
+    continue;  // timing builds (tools/bdist_variants.sh): no mirror phase
+#endif
     __syncthreads();
     // rows j0 + c (c < 256) of the mirror: 8 lanes per row, 16 bytes each
     for (int i = tid; i < kDistThreads * (kDistRows / 4); i += kDistThreads) {
