@@ -501,6 +501,9 @@ def run_carla(ticks, warmup, local, n=None):
             "ms_det": float(np.mean(a[:, 4])), "median_ms_det": float(np.median(a[:, 4])),
             "ms_per_tick_two_streams": float(np.mean(conc)),
             "profiled_tick_gpu_ms": gpu_ms,
+            "profiled_note": "profiled tick: HIP events around every launch serialise the candidate groups and add "
+                             "gaps, so profiled_tick_gpu_ms / kernels_ms_per_tick exceed the wall-clock tick; the "
+                             "rocprofv3 kernel trace (profiles/*_carla_tick_breakdown.txt) is the kernel-time evidence",
             "kernels_ms_per_tick": {k: v[1] for k, v in kt.items()},
             "launches_per_tick": int(sum(v[0] for v in kt.values()))}
 
